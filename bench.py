@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""bench.py — kNN QPS @ recall@10 >= 0.95 (+ build vectors/s) on synthetic 1M x 768 f32 cosine.
+
+Workload = BASELINE.json configs[1]: 1M x 768 f32, cosine, HNSW M=16, efC=128,
+k=10, clustered-latent synthetic data generated in HBM (vsg/datagen.py formulas).
+One step = one HNSW search pass of the query batch (10,000 queries, inputs
+resident in HBM) at the smallest ef whose recall@10 against exact ground truth is
+>= 0.95 (ef swept on a 1,000-query subset).  N > 1: the index is
+row-range sharded (rank r owns rows [r N/G, (r+1) N/G)), every rank searches its
+shard, per-shard top-k is all-gathered over RCCL and k-way merged on every rank
+(SURVEY.md §8e).  Total work is fixed as N grows => "scaling": "strong".
+
+Also reported: build vectors/s (GPU batched HNSW build of the whole index, max over
+ranks), the HBM roofline of the search kernel (algorithmic bytes counted by the
+kernel: distance evaluations x row bytes + adjacency rows x 128 B, per launch, /
+HIP-event time on the launching stream), and the CPU baseline (oracle/ C
+restatement of usearch, SIMD metrics, all host cores or
+SCYLLA_USEARCH_BACKGROUND_THREADS) timed on a bounded sample on rank 0 at N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "vector-store-text_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--metric", default="cos")
+    ap.add_argument("--queries", type=int, default=10_000)
+    ap.add_argument("--gt-queries", type=int, default=1_000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--M", type=int, default=16)
+    ap.add_argument("--efc", type=int, default=128)
+    ap.add_argument("--ef", type=int, default=0, help="fixed ef (0 = sweep for recall >= target)")
+    ap.add_argument("--target-recall", type=float, default=0.95)
+    ap.add_argument("--config", type=int, default=1, help="seed set (BASELINE.json configs index)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    import vsg
+    from vsg import datagen as G
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    bs, qs, ms = G.config_seeds(a.config)
+    lo, hi = rank * a.n // world, (rank + 1) * a.n // world
+    nloc = hi - lo
+    stream = torch.cuda.current_stream()
+
+    # ---- inputs in HBM
+    x = vsg.datagen_device("clustered", nloc, a.dim, bs, ms, start=lo)
+    q = vsg.datagen_device("clustered", a.queries, a.dim, qs, ms)
+    torch.cuda.synchronize()
+
+    # ---- build (timed; not part of the QPS step)
+    index = vsg.Index(a.dim, a.metric, "f32", a.M, a.efc, 128, device=local, seed=0x5EED + rank)
+    index.reserve(nloc)
+    barrier()
+    t0 = time.perf_counter()
+    index.add_device(np.arange(lo, hi, dtype=np.uint64), x, stream=stream)
+    torch.cuda.synchronize()
+    build_s = max_over_ranks(time.perf_counter() - t0)
+    build_vps = a.n / build_s
+    bstats = index.stats()
+
+    def sharded(qt, ef, exact=False):
+        keys, dists = index.search_device(qt, a.k, ef, stream=stream, exact=exact)
+        if world == 1:
+            return keys, dists
+        gk = torch.empty((world,) + tuple(keys.shape), dtype=keys.dtype, device=dev)
+        gd = torch.empty((world,) + tuple(dists.shape), dtype=dists.dtype, device=dev)
+        dist.all_gather_into_tensor(gk, keys)
+        dist.all_gather_into_tensor(gd, dists)
+        return vsg.merge_topk_device(gk, gd, a.k, stream=stream)
+
+    # ---- ground truth (exact, GPU brute force, same sharded merge path)
+    qgt = q[: a.gt_queries].contiguous()
+    gt_keys, _ = sharded(qgt, 0, exact=True)
+    gt = gt_keys.cpu().numpy()
+
+    def recall_of(keys_t):
+        f = keys_t.cpu().numpy()
+        return float(np.mean([len(set(f[i]) & set(gt[i])) / a.k for i in range(gt.shape[0])]))
+
+    # ---- ef selection
+    sweep = []
+    if a.ef:
+        ef = a.ef
+        sweep.append((ef, recall_of(sharded(qgt, ef)[0])))
+    else:
+        ef = None
+        for cand in (16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512):
+            r = recall_of(sharded(qgt, cand)[0])
+            sweep.append((cand, r))
+            if r >= a.target_recall:
+                ef = cand
+                break
+        if ef is None:
+            ef = sweep[-1][0]
+    recall = sweep[-1][1]
+
+    # ---- timed QPS steps
+    for _ in range(a.warmup):
+        sharded(q, ef)
+    index.reset_stats()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    kern_ms = 0.0
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ev0.record(stream)
+        keys, dists = index.search_device(q, a.k, ef, stream=stream)
+        ev1.record(stream)
+        if world > 1:
+            gk = torch.empty((world,) + tuple(keys.shape), dtype=keys.dtype, device=dev)
+            gd = torch.empty((world,) + tuple(dists.shape), dtype=dists.dtype, device=dev)
+            dist.all_gather_into_tensor(gk, keys)
+            dist.all_gather_into_tensor(gd, dists)
+            keys, dists = vsg.merge_topk_device(gk, gd, a.k, stream=stream)
+        torch.cuda.synchronize()
+        kern_ms += ev0.elapsed_time(ev1)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    ms_per_step = 1000.0 * elapsed / a.steps
+    qps = a.queries * a.steps / elapsed
+    st = index.stats()
+    row_bytes = ((a.dim + 3) // 4) * 16
+    alg_bytes = (st["search_distances"] * row_bytes + st["search_adjacency"] * 2 * a.M * 4) / a.steps
+    kern_ms_avg = kern_ms / a.steps
+    achieved = alg_bytes / (kern_ms_avg * 1e-3) / 1e9
+
+    out = {
+        "metric": "kNN QPS @ recall@10>=0.95 (HNSW, 1M x 768 f32 cos)",
+        "value": round(qps, 1),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py), 10k queries/step",
+        "config": {"workload": f"C2: {a.n} x {a.dim} f32 {a.metric} HNSW M={a.M} efC={a.efc} k={a.k}",
+                   "index_rows": a.n, "dim": a.dim, "queries_per_step": a.queries,
+                   "ef": ef, "recall_at_10": round(recall, 4), "ef_sweep": sweep,
+                   "parallelism": f"row-shard x{world}" + (" + RCCL all-gather top-k" if world > 1 else "")},
+        "build_vectors_per_s": round(build_vps, 1),
+        "build_seconds": round(build_s, 3),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "hnsw_search_kernel<64,3,4,float,1>", "kernel_ms": round(kern_ms_avg, 3),
+                     "alg_bytes_per_launch": int(alg_bytes),
+                     "dist_evals_per_query": round(st["search_distances"] / max(1, st["search_queries"]), 1)},
+        "build_stats": {"distance_evals_per_vector": round(bstats["build_distances"] / max(1, nloc), 1),
+                        "batches": bstats["build_batches"]},
+    }
+
+    # ---- CPU baseline (rank 0, N=1 only): oracle/ restatement of usearch
+    if world == 1 and rank == 0 and not a.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(a, index, q, ef, x)
+        if out["cpu_baseline"].get("qps"):
+            out["gpu_over_cpu_qps"] = round(qps / out["cpu_baseline"]["qps"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(a, index, q_t, ef, x_t):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # the checker / CPU baseline only (never the product path)
+
+    O.set_fast_metric(True)
+    threads = int(os.environ.get("SCYLLA_USEARCH_BACKGROUND_THREADS", "0")) or os.cpu_count()
+    res = {"unit": "queries/s", "cores": threads, "kind": "port"}
+    # (1) search QPS: the same graph, exported from HBM, searched by the C restatement
+    g = index.export()
+    h = O.HnswOracle(a.dim, a.metric, a.M, a.efc, ef)
+    h.import_graph(g)
+    del g
+    qh = q_t.cpu().numpy()
+    n = 256
+    t0 = time.perf_counter()
+    h.search(qh[:n], a.k, ef, threads=threads)
+    dt = time.perf_counter() - t0
+    n2 = int(min(len(qh), max(n, n * a.cpu_seconds / max(dt, 1e-6))))
+    t0 = time.perf_counter()
+    h.search(qh[:n2], a.k, ef, threads=threads)
+    dt = time.perf_counter() - t0
+    res["value"] = round(n2 / dt, 1)
+    res["qps"] = res["value"]
+    del h
+    # (2) build vectors/s: concurrent inserts into a fresh index, bounded sample
+    xh = x_t[: 200_000].cpu().numpy()
+    hb = O.HnswOracle(a.dim, a.metric, a.M, a.efc, ef)
+    nb = 20_000
+    t0 = time.perf_counter()
+    hb.add(np.arange(nb), xh[:nb], threads=threads)
+    dt = time.perf_counter() - t0
+    nb2 = int(min(len(xh), max(nb, nb * (1 + a.cpu_seconds / max(dt, 1e-6)))))
+    hb2 = O.HnswOracle(a.dim, a.metric, a.M, a.efc, ef)
+    t0 = time.perf_counter()
+    hb2.add(np.arange(nb2), xh[:nb2], threads=threads)
+    dt = time.perf_counter() - t0
+    res["build_vectors_per_s"] = round(nb2 / dt, 1)
+    res["sample"] = (f"search: {n2} queries at ef={ef} over the GPU-built 1M-row graph exported to host; "
+                     f"build: {nb2} inserts into a fresh index (efC={a.efc}, M={a.M}); "
+                     f"{threads} threads, SIMD f32 metrics")
+    return res
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+/*
+ * vsg.h — C ABI of the MI355X-native ANN index (libvsg.so, gfx950 HIP).
+ *
+ * Drop-in replacement for the usearch-backed index path of the reference
+ * (swasik/vector-store-text @ 2025-06-20, paths relative to /root/reference):
+ * every entry point below replaces one call the reference makes into the
+ * external `usearch` crate from src/index/usearch.rs (cited per function).
+ * Plain pointers and sizes only; no torch / HIP types in the signatures
+ * (streams are passed as void*: a hipStream_t, NULL = the HIP default stream).
+ *
+ * Ownership: the caller owns every host buffer for the duration
+ * of a call; the library copies inputs before returning.  The library owns all
+ * device memory (vectors, graph, keys, tombstones).  The PrimaryKey<->u64 map
+ * stays in the caller (src/index/usearch.rs:109-113); the ABI sees u64 keys.
+ *
+ * Errors: int status, 0 = OK; vsg_last_error() returns a thread-local message
+ * for the last failing call on this thread (the host shim maps it to
+ * anyhow!, like src/index/usearch.rs:259-272, :281-295).
+ *
+ * Threading: add/remove/reserve serialise on an index-wide writer lock (the
+ * reference's RwLock write side, usearch.rs:201-212); search/exact_search take
+ * the shared side and may run concurrently with each other.
+ */
+#ifndef VSG_H
+#define VSG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VSG_OK 0
+#define VSG_EINVAL 1     /* bad argument (dimension mismatch, k == 0, reserved key) */
+#define VSG_ENOMEM 2     /* device or host allocation failed */
+#define VSG_EDUPKEY 3    /* key already present (usearch: duplicate keys not allowed) */
+#define VSG_EDEVICE 4    /* HIP runtime error */
+#define VSG_EUNSUPPORTED 5
+
+#define VSG_METRIC_L2SQ 0 /* sum (a-b)^2, no sqrt */
+#define VSG_METRIC_IP 1   /* 1 - a.b */
+#define VSG_METRIC_COS 2  /* 1 - a.b / (|a| |b|) */
+
+#define VSG_SCALAR_F32 0
+#define VSG_SCALAR_F16 1
+
+#define VSG_NO_KEY UINT64_MAX /* padding key for short result rows */
+
+typedef struct vsg_index vsg_index_t;
+
+/* Mirrors usearch::IndexOptions as built at src/index/usearch.rs:89-96.
+ * The reference leaves `metric` to the crate default, which this ABI makes
+ * explicit.  0 for connectivity / expansion_* means "usearch
+ * default" (16 / 128 / 64), which is what src/db.rs:400-410 passes. */
+typedef struct {
+    uint32_t dimensions;       /* Dimensions, src/lib.rs:146-147 */
+    uint32_t metric;           /* VSG_METRIC_* */
+    uint32_t quantization;     /* VSG_SCALAR_* storage in HBM (ScalarKind::F32, :95) */
+    uint32_t connectivity;     /* Connectivity (M), src/lib.rs:163-164; 0 => 16, max 32 */
+    uint32_t expansion_add;    /* ExpansionAdd (efC), src/lib.rs:181-182; 0 => 128 */
+    uint32_t expansion_search; /* ExpansionSearch (ef), src/lib.rs:199-200; 0 => 64 */
+    int32_t device;            /* HIP device ordinal (one shard per GPU) */
+    uint32_t flags;            /* reserved, 0 */
+    uint64_t seed;             /* level-sampling seed */
+} vsg_index_options_t;
+
+/* Per-index counters for the roofline: every distance
+ * evaluation and adjacency-row read performed by the kernels. */
+typedef struct {
+    uint64_t search_queries;
+    uint64_t search_distances;   /* n_dist, summed over queries */
+    uint64_t search_adjacency;   /* n_adj rows read */
+    uint64_t build_vectors;
+    uint64_t build_distances;
+    uint64_t build_adjacency;
+    uint64_t build_batches;
+} vsg_stats_t;
+
+/* replaces usearch::Index::new(&options) — src/index/usearch.rs:98 */
+int vsg_index_new(const vsg_index_options_t* options, vsg_index_t** out);
+void vsg_index_free(vsg_index_t* index);
+
+/* replaces usearch::Index::reserve — src/index/usearch.rs:99, :206 */
+int vsg_index_reserve(vsg_index_t* index, size_t capacity);
+/* replaces usearch::Index::capacity — src/index/usearch.rs:201 */
+size_t vsg_index_capacity(const vsg_index_t* index);
+/* replaces usearch::Index::size (live, excludes removed) — usearch.rs:202, :309 */
+size_t vsg_index_size(const vsg_index_t* index);
+size_t vsg_index_dimensions(const vsg_index_t* index);
+int vsg_index_contains(const vsg_index_t* index, uint64_t key);
+
+/* replaces usearch::Index::add(key, &[f32]) — src/index/usearch.rs:221.
+ * Batched: n vectors of `dimensions` f32, row-major.  Any live duplicate
+ * (or a duplicate inside the batch) => VSG_EDUPKEY and nothing is inserted.
+ * Grows capacity automatically when needed (the reference reserves ahead,
+ * usearch.rs:200-212; growth here is the same operation). */
+int vsg_index_add(vsg_index_t* index, const uint64_t* keys, const float* vectors, size_t n);
+/* Same, with `vectors` already in device memory (f32, n x dimensions). */
+int vsg_index_add_device(vsg_index_t* index, const uint64_t* keys, const float* vectors_device,
+                         size_t n, void* stream);
+
+/* replaces usearch::Index::remove(key) — src/index/usearch.rs:215, :245.
+ * Tombstones; *n_removed (optional) counts keys that were live. */
+int vsg_index_remove(vsg_index_t* index, const uint64_t* keys, size_t n, size_t* n_removed);
+
+/* replaces usearch::Index::search(&[f32], k) — src/index/usearch.rs:275-277.
+ * HNSW k-NN for nq queries; ef = max(ef ? ef : expansion_search, k).
+ * out_keys / out_distances: nq x k row-major, ascending distance, rows padded
+ * with VSG_NO_KEY / +inf past out_counts[i] (optional). */
+int vsg_index_search(vsg_index_t* index, const float* queries, size_t nq, size_t k, size_t ef,
+                     uint64_t* out_keys, float* out_distances, size_t* out_counts);
+/* Exact brute force over all live vectors (absent in the reference);
+ * same signature; ties broken by insertion slot. */
+int vsg_index_exact_search(vsg_index_t* index, const float* queries, size_t nq, size_t k,
+                           uint64_t* out_keys, float* out_distances, size_t* out_counts);
+
+/* Device-resident variants: queries (f32 nq x dimensions), outputs and counts
+ * (u32, optional) in device memory; enqueued on `stream` (NULL => the HIP
+ * default stream) and NOT synchronised.  Used by bench.py and the multi-GPU
+ * merge.  Concurrent add/remove must not overlap an enqueued search. */
+int vsg_index_search_device(vsg_index_t* index, const float* queries_device, size_t nq, size_t k,
+                            size_t ef, uint64_t* out_keys_device, float* out_distances_device,
+                            uint32_t* out_counts_device, void* stream);
+int vsg_index_exact_search_device(vsg_index_t* index, const float* queries_device, size_t nq,
+                                  size_t k, uint64_t* out_keys_device,
+                                  float* out_distances_device, uint32_t* out_counts_device,
+                                  void* stream);
+
+/* k-way merge of per-shard top-k rows (after an all-gather over xGMI,
+ * SURVEY §8e): parts x nq x k (keys, distances) -> nq x k ascending. */
+int vsg_merge_topk_device(const uint64_t* keys_device, const float* distances_device,
+                          size_t parts, size_t nq, size_t k, uint64_t* out_keys_device,
+                          float* out_distances_device, void* stream);
+
+int vsg_index_stats(const vsg_index_t* index, vsg_stats_t* out);
+int vsg_index_reset_stats(vsg_index_t* index);
+
+/* Graph image, same layout as oracle/vsg_oracle.h "Graph interchange" (and the
+ * HBM layout): vectors as stored (f32 rows of `dimensions`,
+ * normalised for cos), keys, removed flags, levels, level-0 adjacency
+ * slots x 2M, upper_off, upper rows x M.  Sizes via vsg_index_graph_info. */
+int vsg_index_graph_info(const vsg_index_t* index, size_t* slots, size_t* upper_rows,
+                         size_t* connectivity, uint32_t* entry, int* max_level);
+int vsg_index_export(const vsg_index_t* index, float* vectors, uint64_t* keys, uint8_t* removed,
+                     int8_t* levels, uint32_t* adj0, uint32_t* upper_off, uint32_t* upper);
+int vsg_index_import(vsg_index_t* index, size_t slots, const float* vectors,
+                     const uint64_t* keys, const uint8_t* removed, const int8_t* levels,
+                     const uint32_t* adj0, const uint32_t* upper_off, const uint32_t* upper,
+                     size_t upper_rows, uint32_t entry, int max_level);
+
+/* Synthetic inputs generated in HBM (vsg/datagen.py formulas): kind 0 =
+ * clustered-latent, 1 = iid gaussian, 2 = uint8-valued. */
+int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed,
+                       size_t start_row, float* out_device, void* stream);
+
+/* splitmix64 level draw; bit-identical to oracle/vsg_oracle.c */
+int vsg_sample_level(uint64_t seed, uint64_t slot, uint32_t connectivity);
+
+const char* vsg_last_error(void);
+const char* vsg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

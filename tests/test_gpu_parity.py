@@ -1,0 +1,303 @@
+"""GPU parity: libvsg.so (HIP, gfx950) against the oracle and the golden fixtures.
+
+Bar: exact path bit-exact IDs (and distances) on integer data,
+IDs equal except near-ties on float data; HNSW search on an identical graph
+bit-exact vs the oracle on integer data; HNSW GPU build recall within 0.5 %
+of (or better than) the oracle's sequential build at matched ef.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import vsg
+from conftest import GOLDEN, golden_inputs, load_golden
+from vsg import datagen as G
+
+pytestmark = pytest.mark.gpu
+
+NOKEY = np.uint64(2**64 - 1)
+
+
+def recall(found, truth, k):
+    return float(np.mean([len(set(found[i][:k].tolist()) & set(truth[i][:k].tolist())) / k
+                          for i in range(truth.shape[0])]))
+
+
+# ----------------------------------------------------------- exact (brute) --
+
+@pytest.mark.parametrize("name,quant", [("g1_u8_l2sq.npz", "f32"), ("g1_u8_ip.npz", "f32"),
+                                        ("g1_u8_l2sq.npz", "f16"), ("g1_u8_ip.npz", "f16")])
+def test_exact_bitexact_integer_golden(name, quant):
+    g = load_golden(name)
+    x, q = golden_inputs(g)
+    k = int(g["k"])
+    idx = vsg.Index(int(g["dim"]), str(g["metric"]), quant)
+    idx.add(np.arange(x.shape[0]), x)
+    m = idx.exact_search(q, k)
+    assert (m.counts == k).all()
+    np.testing.assert_array_equal(m.keys.astype(np.int64), g["ids"])
+    np.testing.assert_array_equal(m.distances.astype(np.float64), g["dist"])
+
+
+@pytest.mark.parametrize("name", ["g2_cl_ip.npz", "g2_cl_cos.npz", "g2_cl_l2sq.npz", "g3_cl768_cos.npz"])
+def test_exact_float_golden(name):
+    g = load_golden(name)
+    x, q = golden_inputs(g)
+    k = int(g["k"])
+    idx = vsg.Index(int(g["dim"]), str(g["metric"]))
+    idx.add(np.arange(x.shape[0]), x)
+    m = idx.exact_search(q, k)
+    scale = np.maximum(1.0, np.abs(g["dist"]))
+    assert np.max(np.abs(m.distances - g["dist"]) / scale) < 1e-4   # f32 tolerance
+    for i in range(q.shape[0]):
+        if set(m.keys[i].tolist()) != set(g["ids"][i].tolist()):
+            assert g["gap"][i] < 1e-4
+
+
+def test_exact_matches_oracle_with_tombstones_and_keys():
+    x = G.uint8_valued(5000, 24, 21)
+    q = G.uint8_valued(64, 24, 22)
+    keys = np.arange(5000, dtype=np.uint64) * 7 + 3
+    idx = vsg.Index(24, "l2sq")
+    idx.add(keys, x)
+    rm = keys[::5]
+    assert idx.remove(rm) == len(rm)
+    removed = np.zeros(5000, np.uint8)
+    removed[::5] = 1
+    m = idx.exact_search(q, 16)
+    ok, od, _ = O.exact_search("l2sq", x, q, 16, keys=keys, removed=removed)
+    np.testing.assert_array_equal(m.keys, ok)
+    np.testing.assert_array_equal(m.distances, od)
+
+
+# -------------------------------------------------------------- reference KATs --
+
+def _kats():
+    with open(os.path.join(GOLDEN, "kats.json")) as f:
+        return json.load(f)
+
+
+class KeyedIndex:
+    """Host key map (src/index/usearch.rs:174-306) over the GPU index."""
+
+    def __init__(self, dim, metric):
+        self.idx = vsg.Index(dim, metric)
+        self.pk2key, self.key2pk, self.next = {}, {}, 0
+
+    def add_or_replace(self, pk, emb):
+        pk = tuple(pk)
+        if pk in self.pk2key:
+            key = self.pk2key[pk]
+            self.idx.remove([key])
+        else:
+            key = self.next
+            self.next += 1
+            self.pk2key[pk], self.key2pk[key] = key, pk
+        self.idx.add([key], np.array([emb], np.float32))
+
+    def remove(self, pk):
+        key = self.pk2key.pop(tuple(pk), None)
+        if key is not None:
+            self.key2pk.pop(key)
+            self.idx.remove([key])
+
+    def ann(self, emb, limit):
+        m = self.idx.search(np.array([emb], np.float32), limit)
+        c = int(m.counts[0])
+        return [self.key2pk[int(x)] for x in m.keys[0][:c]], m.distances[0][:c]
+
+
+@pytest.mark.parametrize("metric", ["l2sq", "ip"])
+def test_reference_unit_kat(metric):
+    kat = _kats()["unit_actor"]
+    a = KeyedIndex(kat["dimensions"], metric)
+    for st in kat["steps"]:
+        if st["op"] == "add_or_replace":
+            a.add_or_replace(st["pk"], st["embedding"])
+        elif st["op"] == "remove":
+            a.remove(st["pk"])
+        elif st["op"] == "count":
+            assert a.idx.size() == st["expect"]
+        else:
+            pks, dists = a.ann(st["embedding"], st["limit"])
+            assert len(pks) == 1 and len(dists) == 1
+            assert list(pks[0]) == st["expect_pk"]
+
+
+@pytest.mark.parametrize("metric", ["l2sq", "ip"])
+def test_reference_integration_kat(metric):
+    kat = _kats()["integration"]
+    a = KeyedIndex(kat["dimensions"], metric)
+    for pk, emb in kat["rows"]:
+        a.add_or_replace(pk, emb)
+    assert a.idx.size() == kat["count"]
+    pks, _ = a.ann(kat["ann"]["embedding"], kat["ann"]["limit"])
+    assert list(pks[0]) == kat["ann"]["expect_pk"]
+
+
+# ------------------------------------------------------------------- HNSW --
+
+@pytest.mark.parametrize("metric,dim,M", [("l2sq", 32, 8), ("l2sq", 128, 16), ("ip", 64, 16)])
+def test_hnsw_search_same_graph_bitexact(metric, dim, M):
+    """Oracle-built graph imported into HBM: GPU traversal == oracle traversal
+    (integer data => exact distances => identical visiting order)."""
+    n = 6000
+    x = G.uint8_valued(n, dim, 31) / (16.0 if metric == "ip" else 1.0)
+    q = G.uint8_valued(100, dim, 32) / (16.0 if metric == "ip" else 1.0)
+    h = O.HnswOracle(dim, metric, M, 64, 48, seed=5)
+    h.add(np.arange(n), x.astype(np.float32))
+    h.remove(np.arange(0, n, 17))
+    g = h.export()
+    idx = vsg.Index(dim, metric, connectivity=M, expansion_add=64, expansion_search=48, seed=5)
+    idx.import_graph(g)
+    assert idx.size() == h.size()
+    for ef in (10, 48, 100):
+        ok, od, oc = h.search(q, 10, ef)
+        m = idx.search(q, 10, ef)
+        np.testing.assert_array_equal(m.counts, oc)
+        np.testing.assert_array_equal(m.keys, ok)
+        np.testing.assert_array_equal(m.distances, od)
+
+
+@pytest.mark.parametrize("metric,dim,quant", [("l2sq", 64, "f32"), ("cos", 128, "f32"),
+                                              ("ip", 96, "f32"), ("l2sq", 64, "f16")])
+def test_hnsw_gpu_build_recall_vs_oracle(metric, dim, quant):
+    n, nq = 20000, 300
+    bs, qs, ms = G.config_seeds(1)
+    x = G.clustered(n, dim, bs, ms)
+    q = G.clustered(nq, dim, qs, ms)
+    if metric == "ip":  # unit rows so IP ranks like cos
+        x /= np.linalg.norm(x, axis=1, keepdims=True)
+        q /= np.linalg.norm(q, axis=1, keepdims=True)
+    gk, _, _ = O.exact_search(metric, x, q, 10)
+    h = O.HnswOracle(dim, metric, 16, 128, 64, seed=9)
+    h.add(np.arange(n), x, threads=0)
+    idx = vsg.Index(dim, metric, quant, 16, 128, 64, seed=9)
+    idx.add(np.arange(n), x)
+    assert idx.size() == n
+    for ef in (16, 64):
+        rc = recall(h.search(q, 10, ef)[0], gk, 10)
+        rg = recall(idx.search(q, 10, ef).keys, gk, 10)
+        assert rg >= rc - 0.005, (ef, rg, rc)
+
+
+def test_hnsw_incremental_adds_remove_and_readd():
+    dim = 48
+    x = G.uint8_valued(9000, dim, 41)
+    idx = vsg.Index(dim, "l2sq", connectivity=12, expansion_add=96, expansion_search=64)
+    for s in range(0, 9000, 1500):  # several add calls, growing capacity
+        idx.add(np.arange(s, s + 1500), x[s:s + 1500])
+    assert idx.size() == 9000 and idx.capacity() >= 9000
+    with pytest.raises(vsg.DuplicateKeyError):
+        idx.add([10], x[10:11])
+    with pytest.raises(vsg.DuplicateKeyError):
+        idx.add([9001, 9001], x[:2])
+    assert idx.size() == 9000
+    # self-queries find themselves
+    m = idx.search(x[:200], 1)
+    assert (m.keys[:, 0] == np.arange(200)).mean() > 0.99
+    # removal excludes, re-add restores
+    assert idx.remove(np.arange(100)) == 100
+    assert idx.remove(np.arange(100)) == 0
+    m = idx.search(x[:100], 5)
+    assert not np.isin(m.keys, np.arange(100)).any()
+    idx.add(np.arange(100), x[:100])
+    m = idx.search(x[:100], 1)
+    assert (m.keys[:, 0] == np.arange(100)).mean() > 0.97
+    assert idx.size() == 9000
+
+
+def test_edge_cases():
+    idx = vsg.Index(5, "l2sq")
+    m = idx.search(np.zeros((3, 5), np.float32), 4)          # empty index
+    assert (m.counts == 0).all() and (m.keys == NOKEY).all() and np.isinf(m.distances).all()
+    m = idx.exact_search(np.zeros((2, 5), np.float32), 2)
+    assert (m.counts == 0).all()
+    with pytest.raises(vsg.VsgError):
+        idx.search(np.zeros((1, 5), np.float32), 0)          # Limit is NonZeroUsize
+    idx.add([7], np.ones((1, 5), np.float32))
+    m = idx.search(np.zeros((1, 5), np.float32), 3)          # k > size: padded
+    assert int(m.counts[0]) == 1 and int(m.keys[0][0]) == 7 and m.keys[0][1] == NOKEY
+    assert m.distances[0][0] == 5.0
+    m = idx.search(np.zeros((0, 5), np.float32), 3)          # no queries
+    assert m.keys.shape == (0, 3)
+    idx.remove([7])
+    m = idx.search(np.zeros((1, 5), np.float32), 1)          # only tombstones
+    assert int(m.counts[0]) == 0
+
+
+def test_large_scale_properties():
+    """200k x 128 integer data: build, then size-independent properties."""
+    n, dim = 200_000, 128
+    x = G.uint8_valued(n, dim, 51)
+    q = G.uint8_valued(500, dim, 52)
+    idx = vsg.Index(dim, "l2sq", "f16", 16, 128, 64, seed=1)
+    idx.add(np.arange(n), x)
+    ex = idx.exact_search(q, 10)
+    assert (np.diff(ex.distances, axis=1) >= 0).all()
+    m1 = idx.search(q, 10, 128)
+    m2 = idx.search(q, 10, 128)
+    np.testing.assert_array_equal(m1.keys, m2.keys)          # idempotent
+    assert (np.diff(m1.distances, axis=1) >= 0).all()        # sorted
+    assert recall(m1.keys, ex.keys, 10) >= 0.9
+    # every returned distance is the true distance of the returned key
+    d = ((x[m1.keys[:, 0].astype(np.int64)] - q) ** 2).sum(1)
+    np.testing.assert_array_equal(d.astype(np.float32), m1.distances[:, 0])
+
+
+def test_device_api_and_shard_merge():
+    import torch
+    n, dim = 8000, 64
+    x = G.uint8_valued(n, dim, 61)
+    q = G.uint8_valued(128, dim, 62)
+    full = vsg.Index(dim, "l2sq")
+    full.add(np.arange(n), x)
+    truth = full.exact_search(q, 10)
+    # two row-range shards, device-resident inputs, merged with the HIP merge kernel
+    shards = [vsg.Index(dim, "l2sq") for _ in range(2)]
+    xt = torch.from_numpy(x).cuda()
+    qt = torch.from_numpy(q).cuda()
+    for s, sh in enumerate(shards):
+        lo, hi = s * n // 2, (s + 1) * n // 2
+        sh.add_device(np.arange(lo, hi), xt[lo:hi].contiguous())
+    outs = [sh.search_device(qt, 10, exact=True) for sh in shards]
+    keys = torch.stack([o[0] for o in outs])
+    dist = torch.stack([o[1] for o in outs])
+    mk, md = vsg.merge_topk_device(keys, dist, 10)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mk.cpu().numpy().astype(np.uint64), truth.keys)
+    np.testing.assert_array_equal(md.cpu().numpy(), truth.distances)
+
+
+def test_datagen_device_matches_numpy():
+    import torch
+    bs, qs, ms = G.config_seeds(1)
+    a = vsg.datagen_device("clustered", 256, 96, bs, ms, start=1000).cpu().numpy()
+    b = G.clustered(256, 96, bs, ms, start=1000)
+    np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4)
+    u = vsg.datagen_device("uint8", 100, 16, 5).cpu().numpy()
+    np.testing.assert_array_equal(u, G.uint8_valued(100, 16, 5))
+    torch.cuda.synchronize()
+
+
+def test_export_import_gpu_roundtrip():
+    x = G.uint8_valued(3000, 32, 71)
+    q = G.uint8_valued(40, 32, 72)
+    a = vsg.Index(32, "l2sq", connectivity=8, expansion_add=64, expansion_search=32, seed=2)
+    a.add(np.arange(3000), x)
+    a.remove([4, 5])
+    g = a.export()
+    np.testing.assert_array_equal(g["vectors"], x)
+    b = vsg.Index(32, "l2sq", connectivity=8, expansion_add=64, expansion_search=32, seed=2)
+    b.import_graph(g)
+    ma, mb = a.search(q, 10), b.search(q, 10)
+    np.testing.assert_array_equal(ma.keys, mb.keys)
+    # the oracle searching the GPU-built graph agrees with the GPU bit-exactly
+    h = O.HnswOracle(32, "l2sq", 8, 64, 32, seed=2)
+    h.import_graph(g)
+    ok, od, _ = h.search(q, 10, 32)
+    np.testing.assert_array_equal(ma.keys, ok)
+    np.testing.assert_array_equal(ma.distances, od)

@@ -1,0 +1,454 @@
+// hnsw.hip — HNSW search and batched build kernels for gfx950 (CDNA4).
+//
+// Semantics follow the CPU restatement oracle/vsg_oracle.c (usearch
+// index.hpp, restated): greedy descent on levels > 0, "expand the best
+// unexpanded entry of the (distance, slot)-sorted top-ef list" on the beam
+// level, heuristic (refine) neighbour selection, reverse links appended while
+// there is room and re-selected with the heuristic otherwise.  Reference call
+// sites: usearch::Index::search (src/index/usearch.rs:275-277) and
+// usearch::Index::add (src/index/usearch.rs:221).
+//
+// One wave64 per query / inserted node; all per-wave state in LDS (vsg_device.hpp).
+// Base rows and adjacency are read straight from HBM into VGPRs (HBM-bound
+// traversal).
+#include <hip/hip_runtime.h>
+
+#include "vsg_device.hpp"
+#include "vsg_dispatch.hpp"
+#include "vsg_kernels.hpp"
+
+namespace vsg {
+
+static __host__ __device__ inline int hash_size_for(int ef) {
+    int h = 1024;
+    while (h < 32 * ef && h < 16384) h <<= 1;
+    return h;
+}
+
+size_t search_lds_bytes(int ef) {
+    return (size_t)hash_size_for(ef) * 4 + (size_t)ef * 16 + 64 * 4 * 4;
+}
+
+size_t insert_lds_bytes(int efc) { return search_lds_bytes(efc) + 64 * 4 * 2; }
+
+static __device__ inline GraphDev to_dev(const DevGraph& g) {
+    GraphDev d;
+    d.vecs = g.vecs;
+    d.row_bytes = g.row_bytes;
+    d.nchunks = g.nchunks;
+    d.adj0 = g.adj0;
+    d.upper_off = g.upper_off;
+    d.upper = g.upper;
+    d.M = g.M;
+    d.M0 = g.M0;
+    return d;
+}
+
+struct WaveLds {
+    Visited vis;
+    List list;
+    float* sd;
+    uint32_t* si;
+    uint32_t* todo;
+    float* tdist;
+    uint32_t* sel;
+    float* seld;
+};
+
+static __device__ inline WaveLds carve(uint8_t* smem, int cap, bool with_sel) {
+    WaveLds w;
+    const int hs = hash_size_for(cap);
+    uint8_t* p = smem;
+    w.vis.tab = reinterpret_cast<uint32_t*>(p);
+    w.vis.mask = (uint32_t)hs - 1;
+    p += (size_t)hs * 4;
+    w.list.d0 = reinterpret_cast<float*>(p);
+    p += (size_t)cap * 4;
+    w.list.d1 = reinterpret_cast<float*>(p);
+    p += (size_t)cap * 4;
+    w.list.i0 = reinterpret_cast<uint32_t*>(p);
+    p += (size_t)cap * 4;
+    w.list.i1 = reinterpret_cast<uint32_t*>(p);
+    p += (size_t)cap * 4;
+    w.list.cap = cap;
+    w.list.cur = 0;
+    w.list.size = 0;
+    w.sd = reinterpret_cast<float*>(p);
+    p += 256;
+    w.si = reinterpret_cast<uint32_t*>(p);
+    p += 256;
+    w.todo = reinterpret_cast<uint32_t*>(p);
+    p += 256;
+    w.tdist = reinterpret_cast<float*>(p);
+    p += 256;
+    if (with_sel) {
+        w.sel = reinterpret_cast<uint32_t*>(p);
+        p += 256;
+        w.seld = reinterpret_cast<float*>(p);
+        p += 256;
+    } else {
+        w.sel = nullptr;
+        w.seld = nullptr;
+    }
+    return w;
+}
+
+// distance from q to a single slot (result in all lanes)
+template <int G, int VM, int U, typename T, int MET>
+__device__ inline float dist_one(const GraphDev& g, const QReg<G, VM, T>& q, uint32_t s, WaveLds& w) {
+    if (lane_id() == 0) w.todo[0] = s;
+    wave_sync();
+    rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, 1, q, w.tdist);
+    wave_sync();
+    const float d = w.tdist[0];
+    wave_sync();
+    return d;
+}
+
+// usearch search_for_one_ restated (oracle greedy()): move to the best
+// neighbour (lexicographic (distance, slot)) until none improves.
+template <int G, int VM, int U, typename T, int MET>
+__device__ void greedy_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t& cur,
+                             float& dcur, WaveLds& w, uint64_t& ndist, uint64_t& nadj) {
+    const int lane = lane_id();
+    const int m = l == 0 ? g.M0 : g.M;
+    for (;;) {
+        const uint32_t* row = g.row(cur, l);
+        const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
+        const bool ok = nb != VSG_EMPTY;
+        const uint64_t mask = __ballot(ok);
+        const int cnt = popc64(mask);
+        ++nadj;
+        if (ok) w.todo[lanes_below(mask)] = nb;
+        wave_sync();
+        if (cnt == 0) break;
+        rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
+        wave_sync();
+        ndist += (uint64_t)cnt;
+        float d = lane < cnt ? w.tdist[lane] : __builtin_inff();
+        uint32_t id = lane < cnt ? w.todo[lane] : VSG_EMPTY;
+        wave_sync();
+        wave_argmin(d, id);
+        if (cand_less(d, id, dcur, cur)) {
+            cur = id;
+            dcur = d;
+        } else {
+            break;
+        }
+    }
+}
+
+// usearch search_to_find_in_base_ restated (oracle beam()).
+template <int G, int VM, int U, typename T, int MET>
+__device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t ep, float dep,
+                           WaveLds& w, uint64_t& ndist, uint64_t& nadj) {
+    const int lane = lane_id();
+    const int m = l == 0 ? g.M0 : g.M;
+    w.vis.clear();
+    List& L = w.list;
+    L.cur = 0;
+    L.size = 1;
+    if (lane == 0) {
+        bool unrec;
+        w.vis.insert(ep, unrec);
+        L.d0[0] = dep;
+        L.i0[0] = ep;
+    }
+    wave_sync();
+    for (;;) {
+        const int p = L.first_unexpanded();
+        if (p < 0) break;
+        const uint32_t node = L.I()[p] & VSG_ID_MASK;
+        wave_sync();
+        if (lane == 0) L.I()[p] = node | VSG_EXP_BIT;
+        const uint32_t* row = g.row(node, l);
+        const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
+        ++nadj;
+        bool fresh = false, unrec = false;
+        if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, unrec);
+        const uint64_t mask = __ballot(fresh);
+        const bool any_unrec = __ballot(unrec) != 0;
+        const int cnt = popc64(mask);
+        if (fresh) w.todo[lanes_below(mask)] = nb;
+        wave_sync();
+        if (cnt == 0) continue;
+        rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
+        wave_sync();
+        ndist += (uint64_t)cnt;
+        const bool valid = lane < cnt;
+        const float cd = valid ? w.tdist[lane] : 0.f;
+        const uint32_t ci = valid ? w.todo[lane] : 0u;
+        wave_sync();
+        L.merge(valid, cd, ci, any_unrec, w.sd, w.si);
+    }
+}
+
+// usearch refine_ restated (oracle select_heuristic()): walk the sorted list,
+// keep c unless a kept r has dist(c, r) < dist(c, base).  Returns #kept.
+template <int G, int VM, int U, typename T, int MET>
+__device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uint64_t& ndist) {
+    constexpr int BLK = (64 / G) * U;
+    const int lane = lane_id();
+    List& L = w.list;
+    int kept = 0;
+    for (int i = 0; i < n && kept < m; ++i) {
+        const uint32_t c = L.I()[i] & VSG_ID_MASK;
+        const float cdist = L.D()[i];
+        QReg<G, VM, T> cq;
+        cq.load(g.vec(c), g.nchunks);
+        bool good = true;
+        for (int b = 0; b < kept; b += BLK) {
+            const int cnt = min(BLK, kept - b);
+            rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.sel + b, cnt, cq, w.tdist);
+            wave_sync();
+            ndist += (uint64_t)cnt;
+            const bool bad = lane < cnt && w.tdist[lane] < cdist;
+            const uint64_t bm = __ballot(bad);
+            wave_sync();
+            if (bm) {
+                good = false;
+                break;
+            }
+        }
+        if (good) {
+            if (lane == 0) {
+                w.sel[kept] = c;
+                w.seld[kept] = cdist;
+            }
+            ++kept;
+            wave_sync();
+        }
+    }
+    return kept;
+}
+
+// ------------------------------------------------------------------ search --
+
+template <int G, int VM, int U, typename T, int MET>
+__global__ __launch_bounds__(64) void hnsw_search_kernel(SearchParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int qi = blockIdx.x;
+    const int lane = lane_id();
+    const GraphDev g = to_dev(p.g);
+    WaveLds w = carve(smem, p.ef, false);
+    uint64_t ndist = 0, nadj = 0;
+    int count = 0;
+    uint64_t* ok = p.out_keys + (size_t)qi * p.k;
+    float* od = p.out_dist + (size_t)qi * p.k;
+    if (p.entry != VSG_EMPTY) {
+        QReg<G, VM, T> q;
+        q.load(p.queries + (size_t)qi * g.row_bytes, g.nchunks);
+        uint32_t cur = p.entry;
+        float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
+        ++ndist;
+        for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+        beam_level<G, VM, U, T, MET>(g, q, 0, cur, dcur, w, ndist, nadj);
+        const List& L = w.list;
+        for (int r = 0; r < L.size && count < p.k; r += 64) {
+            const int i = r + lane;
+            const bool valid = i < L.size;
+            const uint32_t id = valid ? (L.I()[i] & VSG_ID_MASK) : 0u;
+            const bool alive = valid && !(p.flags[id] & 1);
+            const uint64_t m = __ballot(alive);
+            const int pos = count + lanes_below(m);
+            if (alive && pos < p.k) {
+                ok[pos] = p.keys[id];
+                od[pos] = L.D()[i];
+            }
+            count += popc64(m);
+        }
+        if (count > p.k) count = p.k;
+    }
+    for (int j = count + lane; j < p.k; j += 64) {
+        ok[j] = ~0ull;
+        od[j] = __builtin_inff();
+    }
+    if (lane == 0) {
+        if (p.out_counts) p.out_counts[qi] = (uint32_t)count;
+        if (p.stats) {
+            atomicAdd(&p.stats[0], (unsigned long long)ndist);
+            atomicAdd(&p.stats[1], (unsigned long long)nadj);
+            atomicAdd(&p.stats[2], 1ull);
+        }
+    }
+}
+
+// ------------------------------------------------------------ build: fwd --
+// One wave per new node of the batch: descend, beam with efC per level,
+// select M_l neighbours, write the node's own rows and emit (level, v, u)
+// reverse-link pairs at the node's pre-assigned offset (no atomics).
+
+template <int G, int VM, int U, typename T, int MET>
+__global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int bi = blockIdx.x;
+    const int lane = lane_id();
+    const GraphDev g = to_dev(p.g);
+    WaveLds w = carve(smem, p.efc, true);
+    const uint32_t node = p.base_slot + (uint32_t)bi;
+    const int L = p.levels[bi];
+    uint64_t ndist = 0, nadj = 0;
+    QReg<G, VM, T> q;
+    q.load(g.vec(node), g.nchunks);
+    uint32_t cur = p.entry;
+    float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
+    ++ndist;
+    for (int l = p.max_level; l > L; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+    uint32_t pos = p.pair_off[bi];
+    for (int l = min(L, p.max_level); l >= 0; --l) {
+        beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+        const int m = l == 0 ? g.M0 : g.M;
+        const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, m, ndist);
+        uint32_t* row = g.row(node, l);
+        if (lane < m) row[lane] = lane < nsel ? w.sel[lane] : VSG_EMPTY;
+        if (lane < nsel) {
+            const uint64_t key = ((uint64_t)l << PAIR_L_SHIFT) | ((uint64_t)w.sel[lane] << PAIR_V_SHIFT) |
+                                 (uint64_t)node;
+            p.pair_keys[pos + lane] = key;
+            p.pair_vals[pos + lane] = __float_as_uint(w.seld[lane]);
+        }
+        pos += (uint32_t)nsel;
+        cur = w.list.I()[0] & VSG_ID_MASK;
+        dcur = w.list.D()[0];
+        wave_sync();
+    }
+    if (lane == 0 && p.stats) {
+        atomicAdd(&p.stats[3], (unsigned long long)ndist);
+        atomicAdd(&p.stats[4], (unsigned long long)nadj);
+    }
+}
+
+// ------------------------------------------------------------ build: rev --
+// Pairs sorted by (level, v, u).  Persistent waves scan contiguous chunks for
+// segment heads; each segment (level, v) is merged into v's row: append while
+// there is room, else heuristic re-selection over existing + incoming.
+
+template <int G, int VM, int U, typename T, int MET>
+__global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = lane_id();
+    const GraphDev g = to_dev(p.g);
+    const int cap = 2 * g.M0 > 64 ? 2 * g.M0 : 64;
+    WaveLds w = carve(smem, cap, true);
+    uint64_t ndist = 0, nadj = 0;
+    const size_t nw = gridDim.x;
+    size_t chunk = (p.npairs + nw - 1) / nw;
+    chunk = (chunk + 63) & ~(size_t)63;
+    const size_t beg = (size_t)blockIdx.x * chunk;
+    const size_t end = min(beg + chunk, p.npairs);
+    for (size_t i0 = beg; i0 < end; i0 += 64) {
+        const size_t i = i0 + lane;
+        const uint64_t key = i < end ? p.keys[i] : ~0ull;
+        const uint64_t prev = (i < end && i > 0) ? p.keys[i - 1] : ~0ull;
+        const bool head = key != ~0ull && (i == 0 || (key >> PAIR_V_SHIFT) != (prev >> PAIR_V_SHIFT));
+        uint64_t heads = __ballot(head);
+        while (heads) {
+            const int hl = __builtin_ctzll(heads);
+            heads &= heads - 1;
+            const size_t h = i0 + hl;
+            const uint64_t hkey = p.keys[h];
+            const uint64_t seg = hkey >> PAIR_V_SHIFT;
+            const int l = (int)(hkey >> PAIR_L_SHIFT);
+            const uint32_t v = (uint32_t)((hkey >> PAIR_V_SHIFT) & PAIR_ID_MASK);
+            // segment end
+            size_t e = h;
+            for (;;) {
+                const size_t j = e + lane;
+                const bool same = j < p.npairs && (p.keys[j] >> PAIR_V_SHIFT) == seg;
+                const uint64_t nm = __ballot(!same);
+                if (nm) {
+                    e += __builtin_ctzll(nm);
+                    break;
+                }
+                e += 64;
+            }
+            const int nin = (int)(e - h);
+            const int m = l == 0 ? g.M0 : g.M;
+            uint32_t* row = g.row(v, l);
+            const uint32_t x = lane < m ? row[lane] : VSG_EMPTY;
+            ++nadj;
+            const uint64_t xm = __ballot(x != VSG_EMPTY);
+            const int ne = popc64(xm);
+            if (ne + nin <= m) {
+                for (int t = lane; t < nin; t += 64) row[ne + t] = (uint32_t)(p.keys[h + t] & PAIR_ID_MASK);
+                continue;
+            }
+            QReg<G, VM, T> q;
+            q.load(g.vec(v), g.nchunks);
+            List& L = w.list;
+            L.cur = 0;
+            L.size = 0;
+            if (x != VSG_EMPTY) w.todo[lanes_below(xm)] = x;
+            wave_sync();
+            rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, ne, q, w.tdist);
+            wave_sync();
+            ndist += (uint64_t)ne;
+            {
+                const bool valid = lane < ne;
+                const float cd = valid ? w.tdist[lane] : 0.f;
+                const uint32_t ci = valid ? w.todo[lane] : 0u;
+                wave_sync();
+                L.merge(valid, cd, ci, false, w.sd, w.si);
+            }
+            for (int t = 0; t < nin; t += 64) {
+                const bool valid = t + lane < nin;
+                const size_t idx = h + t + lane;
+                const float cd = valid ? __uint_as_float(p.vals[idx]) : 0.f;
+                const uint32_t ci = valid ? (uint32_t)(p.keys[idx] & PAIR_ID_MASK) : 0u;
+                L.merge(valid, cd, ci, false, w.sd, w.si);
+            }
+            const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, L.size, m, ndist);
+            if (lane < m) row[lane] = lane < nsel ? w.sel[lane] : VSG_EMPTY;
+            wave_sync();
+        }
+    }
+    if (lane == 0 && p.stats) {
+        atomicAdd(&p.stats[3], (unsigned long long)ndist);
+        atomicAdd(&p.stats[4], (unsigned long long)nadj);
+    }
+}
+
+// ------------------------------------------------------------------ launch --
+
+bool shape_supported(int nchunks) { return nchunks >= 1 && nchunks <= 1024; }
+
+hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s) {
+    if (p.nq <= 0) return hipSuccess;
+    const size_t lds = search_lds_bytes(p.ef);
+    hipError_t err = hipSuccess;
+    dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+        auto kern = VSG_KERNEL_OF(hnsw_search_kernel, sh, tt, mt);
+        if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3(p.nq), dim3(64), lds, s, p);
+        err = hipGetLastError();
+    });
+    return err;
+}
+
+hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s) {
+    if (p.nnodes <= 0) return hipSuccess;
+    const size_t lds = insert_lds_bytes(p.efc);
+    hipError_t err = hipSuccess;
+    dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+        auto kern = VSG_KERNEL_OF(hnsw_insert_kernel, sh, tt, mt);
+        if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3(p.nnodes), dim3(64), lds, s, p);
+        err = hipGetLastError();
+    });
+    return err;
+}
+
+hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s) {
+    if (p.npairs == 0) return hipSuccess;
+    const int cap = 2 * p.g.M0 > 64 ? 2 * p.g.M0 : 64;
+    const size_t lds = insert_lds_bytes(cap);
+    hipError_t err = hipSuccess;
+    dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+        auto kern = VSG_KERNEL_OF(hnsw_reverse_kernel, sh, tt, mt);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, p);
+        err = hipGetLastError();
+    });
+    return err;
+}
+
+}  // namespace vsg

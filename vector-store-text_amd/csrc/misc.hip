@@ -1,0 +1,169 @@
+// misc.hip — row preparation (f32 -> storage type, cos normalisation),
+// tombstone scatter and the HBM synthetic-data generator.
+#include <hip/hip_runtime.h>
+
+#include "vsg_device.hpp"
+#include "vsg_kernels.hpp"
+
+namespace vsg {
+
+// One wave per row.  Cos rows are stored unit-normalised (x / |x|) so the
+// traversal kernels evaluate cos as 1 - dot.
+template <typename T>
+__global__ __launch_bounds__(256) void prepare_kernel(const float* __restrict__ in, size_t n, int dim,
+                                                      int normalize, uint8_t* __restrict__ out,
+                                                      size_t row_bytes) {
+    const size_t row = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= n) return;
+    const float* x = in + row * (size_t)dim;
+    T* y = reinterpret_cast<T*>(out + row * row_bytes);
+    float nrm = 1.f;
+    if (normalize) {
+        float s = 0.f;
+        for (int j = lane; j < dim; j += 64) s += x[j] * x[j];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        nrm = sqrtf(s);
+    }
+    const int padded = (int)(row_bytes / sizeof(T));
+    for (int j = lane; j < padded; j += 64) {
+        float v = 0.f;
+        if (j < dim) v = (normalize && nrm > 0.f) ? x[j] / nrm : (normalize ? 0.f : x[j]);
+        y[j] = (T)v;
+    }
+}
+
+template <typename T>
+__global__ void unprepare_kernel(const uint8_t* __restrict__ in, size_t n, int dim, size_t row_bytes,
+                                 float* __restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * (size_t)dim) return;
+    const size_t r = i / dim;
+    const int j = (int)(i % dim);
+    out[i] = (float)reinterpret_cast<const T*>(in + r * row_bytes)[j];
+}
+
+hipError_t launch_prepare(Storage st, const float* in, size_t n, int dim, bool normalize, uint8_t* out,
+                          size_t row_bytes, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 3) / 4));
+    if (st == ST_F32)
+        hipLaunchKernelGGL(prepare_kernel<float>, grid, dim3(256), 0, s, in, n, dim, normalize ? 1 : 0, out, row_bytes);
+    else
+        hipLaunchKernelGGL(prepare_kernel<_Float16>, grid, dim3(256), 0, s, in, n, dim, normalize ? 1 : 0, out,
+                           row_bytes);
+    return hipGetLastError();
+}
+
+hipError_t launch_unprepare(Storage st, const uint8_t* in, size_t n, int dim, size_t row_bytes, float* out,
+                            hipStream_t s) {
+    const size_t tot = n * (size_t)dim;
+    if (tot == 0) return hipSuccess;
+    const dim3 grid((unsigned)((tot + 255) / 256));
+    if (st == ST_F32)
+        hipLaunchKernelGGL(unprepare_kernel<float>, grid, dim3(256), 0, s, in, n, dim, row_bytes, out);
+    else
+        hipLaunchKernelGGL(unprepare_kernel<_Float16>, grid, dim3(256), 0, s, in, n, dim, row_bytes, out);
+    return hipGetLastError();
+}
+
+__global__ void set_flags_kernel(uint8_t* flags, const uint32_t* slots, size_t n, uint8_t value) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flags[slots[i]] = value;
+}
+
+hipError_t launch_set_flags(uint8_t* flags, const uint32_t* slots, size_t n, uint8_t value, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(set_flags_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, flags, slots, n,
+                       value);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- datagen --
+// Same formulas and stream tags as vector-store-text_amd/vsg/datagen.py.
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+constexpr uint64_t TAG_CLUSTER = 0x436C7573, TAG_LATENT = 0x4C6174, TAG_NOISE = 0x4E6F6973,
+                   TAG_CENTRE = 0x43656E74, TAG_PROJ = 0x50726F6A, TAG_U8 = 0x55380000;
+constexpr int N_CENTRES = 1024, LATENT = 64;
+
+__device__ inline double uniform01(uint64_t base, uint64_t idx) {
+    const uint64_t r = splitmix64(base + idx);
+    return ((double)(r >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+}
+
+__device__ inline float normal_at(uint64_t base, uint64_t idx) {
+    const double u1 = uniform01(base, 2 * idx);
+    const double u2 = uniform01(base, 2 * idx + 1);
+    return (float)(sqrt(-2.0 * log(u1)) * cos(2.0 * 3.141592653589793 * u2));
+}
+
+__global__ void gen_normal_kernel(uint64_t base, size_t count, float scale, float* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) out[i] = normal_at(base, i) / scale;
+}
+
+__global__ __launch_bounds__(64) void gen_clustered_kernel(size_t n, int dim, uint64_t seed, size_t start,
+                                                           const float* __restrict__ w,
+                                                           const float* __restrict__ centres,
+                                                           float* __restrict__ out) {
+    __shared__ float lat[LATENT];
+    const size_t r = blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint64_t row = start + r;
+    const uint64_t cl = splitmix64(splitmix64(seed ^ TAG_CLUSTER) + row) % N_CENTRES;
+    const uint64_t lbase = splitmix64(seed ^ TAG_LATENT);
+    lat[lane] = centres[cl * LATENT + lane] + 0.5f * normal_at(lbase, row * LATENT + lane);
+    __syncthreads();
+    const uint64_t nbase = splitmix64(seed ^ TAG_NOISE);
+    for (int j = lane; j < dim; j += 64) {
+        float acc = 0.f;
+        for (int l = 0; l < LATENT; ++l) acc += lat[l] * w[(size_t)l * dim + j];
+        out[r * dim + j] = acc + 0.05f * normal_at(nbase, row * (uint64_t)dim + j);
+    }
+}
+
+__global__ void gen_gauss_kernel(size_t n, int dim, uint64_t seed, size_t start, float* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * (size_t)dim) return;
+    const uint64_t nbase = splitmix64(seed ^ TAG_NOISE);
+    out[i] = normal_at(nbase, start * (uint64_t)dim + i);
+}
+
+__global__ void gen_u8_kernel(size_t n, int dim, uint64_t seed, size_t start, float* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * (size_t)dim) return;
+    const uint64_t b = splitmix64(seed ^ TAG_U8);
+    out[i] = (float)(splitmix64(b + start * (uint64_t)dim + i) % 256);
+}
+
+hipError_t launch_datagen(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed, size_t start_row,
+                          float* out, float* scratch_w, float* scratch_c, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const size_t tot = n * dim;
+    if (kind == 0) {
+        const size_t nw = (size_t)LATENT * dim, ncen = (size_t)N_CENTRES * LATENT;
+        hipLaunchKernelGGL(gen_normal_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s,
+                           splitmix64(model_seed ^ TAG_PROJ), nw, 8.0f, scratch_w);
+        hipLaunchKernelGGL(gen_normal_kernel, dim3((unsigned)((ncen + 255) / 256)), dim3(256), 0, s,
+                           splitmix64(model_seed ^ TAG_CENTRE), ncen, 1.0f, scratch_c);
+        hipLaunchKernelGGL(gen_clustered_kernel, dim3((unsigned)n), dim3(64), 0, s, n, (int)dim, seed, start_row,
+                           scratch_w, scratch_c, out);
+    } else if (kind == 1) {
+        hipLaunchKernelGGL(gen_gauss_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, n, (int)dim,
+                           seed, start_row, out);
+    } else {
+        hipLaunchKernelGGL(gen_u8_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, n, (int)dim, seed,
+                           start_row, out);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace vsg

@@ -1,0 +1,308 @@
+// vsg_device.hpp — wave64 device primitives shared by the HNSW / exact kernels.
+//
+// Execution model: one wave64 = one workgroup = one query (search)
+// or one inserted node (build).  All per-wave state lives in LDS:
+//   visited hash (u32, open addressing), a (distance, slot) list sorted
+//   lexicographically (double-buffered for merges), candidate scratch.
+// Base rows are fetched straight to VGPRs in 16-B chunks: a row is split over
+// G lanes (G in {4..64}), each lane holds VM chunks, 64/G rows per pass, U
+// passes issued back-to-back before any arithmetic so 8-16 loads per lane are
+// in flight; partial sums are reduced across the G lanes with xor shuffles.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VSG_EMPTY 0xFFFFFFFFu
+#define VSG_EXP_BIT 0x80000000u
+#define VSG_ID_MASK 0x7FFFFFFFu
+
+namespace vsg {
+
+enum { MET_L2 = 0, MET_DOT = 1 };
+
+// elements per 16-byte chunk
+template <typename T> struct ChunkT;
+template <> struct ChunkT<float> { static constexpr int E = 4; };
+template <> struct ChunkT<_Float16> { static constexpr int E = 8; };
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+
+template <typename T>
+__device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ row, int c,
+                                           float (&out)[ChunkT<T>::E]) {
+    const uint4 raw = *reinterpret_cast<const uint4*>(row + (size_t)c * 16);
+    if constexpr (sizeof(T) == 4) {
+        out[0] = __uint_as_float(raw.x);
+        out[1] = __uint_as_float(raw.y);
+        out[2] = __uint_as_float(raw.z);
+        out[3] = __uint_as_float(raw.w);
+    } else {
+        half8_t h = __builtin_bit_cast(half8_t, raw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) out[e] = (float)h[e];
+    }
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ void wave_sync() {
+    // single-wave workgroups: orders this wave's LDS traffic across lanes
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ bool cand_less(float da, uint32_t ia, float db, uint32_t ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+__device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
+
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+template <typename X> __device__ __forceinline__ X readlane(X x, int l) {
+    if constexpr (sizeof(X) == 4) {
+        return __builtin_bit_cast(X, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+    } else {
+        static_assert(sizeof(X) == 4, "32-bit only");
+    }
+}
+
+// Lexicographic (d, id) minimum across the wave; result in all lanes.
+__device__ __forceinline__ void wave_argmin(float& d, uint32_t& id) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float od = __shfl_xor(d, o);
+        uint32_t oi = (uint32_t)__shfl_xor((int)id, o);
+        if (cand_less(od, oi, d, id)) {
+            d = od;
+            id = oi;
+        }
+    }
+}
+
+// Query / candidate register image: lane (sub, sl) holds chunks v*G + sl.
+template <int G, int VM, typename T> struct QReg {
+    static constexpr int E = ChunkT<T>::E;
+    float x[VM][E];
+
+    __device__ __forceinline__ void load(const uint8_t* __restrict__ row, int nchunks) {
+        const int sl = lane_id() % G;
+#pragma unroll
+        for (int v = 0; v < VM; ++v) {
+            const int c = v * G + sl;
+            const int cc = c < nchunks ? c : nchunks - 1;
+            load_chunk<T>(row, cc, x[v]);
+            if (c >= nchunks) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) x[v][e] = 0.f;
+            }
+        }
+    }
+};
+
+// Distances from the register image q to `count` rows listed in ids[] (LDS),
+// written to out[] (LDS).  Wave-uniform count.  Returns nothing; out[r] holds
+// the metric distance (l2sq, or 1 - dot).
+template <int G, int VM, int U, typename T, int MET>
+__device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size_t row_bytes,
+                                          int nchunks, const uint32_t* ids, int count,
+                                          const QReg<G, VM, T>& q, float* out) {
+    constexpr int R = 64 / G;
+    constexpr int E = ChunkT<T>::E;
+    const int lane = lane_id();
+    const int sub = lane / G;
+    const int sl = lane % G;
+    for (int base = 0; base < count; base += R * U) {
+        float buf[U][VM][E];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = base + u * R + sub;
+            const int rr = r < count ? r : count - 1;
+            const uint8_t* row = vecs + (size_t)ids[rr] * row_bytes;
+#pragma unroll
+            for (int v = 0; v < VM; ++v) {
+                const int c = v * G + sl;
+                load_chunk<T>(row, c < nchunks ? c : nchunks - 1, buf[u][v]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float acc = 0.f;
+#pragma unroll
+            for (int v = 0; v < VM; ++v) {
+                const bool live = (v * G + sl) < nchunks;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    float t;
+                    if constexpr (MET == MET_L2) {
+                        const float df = buf[u][v][e] - q.x[v][e];
+                        t = df * df;
+                    } else {
+                        t = buf[u][v][e] * q.x[v][e];
+                    }
+                    acc += live ? t : 0.f;
+                }
+            }
+#pragma unroll
+            for (int o = G / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+            const int r = base + u * R + sub;
+            if (sl == 0 && r < count) out[r] = (MET == MET_L2) ? acc : 1.f - acc;
+        }
+    }
+}
+
+// ----------------------------------------------------------------- visited --
+
+struct Visited {
+    uint32_t* tab;
+    uint32_t mask;  // size - 1 (power of two)
+
+    __device__ __forceinline__ void clear() {
+        const int lane = lane_id();
+        uint4* t4 = reinterpret_cast<uint4*>(tab);
+        const uint32_t n4 = (mask + 1) / 4;
+        for (uint32_t i = lane; i < n4; i += 64) t4[i] = make_uint4(VSG_EMPTY, VSG_EMPTY, VSG_EMPTY, VSG_EMPTY);
+        wave_sync();
+    }
+
+    // true if id was not present (inserted now, or the table could not record
+    // it: then `unrecorded` is set and the caller de-duplicates).
+    __device__ __forceinline__ bool insert(uint32_t id, bool& unrecorded) {
+        uint32_t h = (id * 2654435761u) & mask;
+        unrecorded = false;
+#pragma unroll 1
+        for (int p = 0; p < 32; ++p) {
+            const uint32_t old = atomicCAS(&tab[h], VSG_EMPTY, id);
+            if (old == VSG_EMPTY) return true;
+            if (old == id) return false;
+            h = (h + 1) & mask;
+        }
+        unrecorded = true;
+        return true;
+    }
+};
+
+// ------------------------------------------------------------- sorted list --
+// (distance, slot) ascending; slot high bit = "expanded".  cap <= 1024.
+
+struct List {
+    float* d0;
+    float* d1;
+    uint32_t* i0;
+    uint32_t* i1;
+    int cur;
+    int size;
+    int cap;
+
+    // explicit selects: a runtime-indexed pointer array would live in scratch
+    __device__ __forceinline__ float* D() const { return cur ? d1 : d0; }
+    __device__ __forceinline__ uint32_t* I() const { return cur ? i1 : i0; }
+    __device__ __forceinline__ float* Dn() const { return cur ? d0 : d1; }
+    __device__ __forceinline__ uint32_t* In() const { return cur ? i0 : i1; }
+
+    // first entry not yet expanded, or -1
+    __device__ __forceinline__ int first_unexpanded() const {
+        const int lane = lane_id();
+        for (int r = 0; r < size; r += 64) {
+            const int i = r + lane;
+            const bool un = i < size && !(I()[i] & VSG_EXP_BIT);
+            const uint64_t m = __ballot(un);
+            if (m) return r + __builtin_ctzll(m);
+        }
+        return -1;
+    }
+
+    // #entries strictly less than (cd, ci), binary search in LDS
+    __device__ __forceinline__ int lower_bound(float cd, uint32_t ci) const {
+        int lo = 0, hi = size;
+        const float* dd = D();
+        const uint32_t* ii = I();
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (cand_less(dd[mid], ii[mid] & VSG_ID_MASK, cd, ci)) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    }
+
+    // Merge one candidate per lane (valid lanes only).  Candidates must have
+    // distinct ids that are not in the list unless `maybe_dup` is set for them.
+    // sd/si: 64-entry LDS scratch.
+    __device__ void merge(bool valid, float cd, uint32_t ci, bool maybe_dup, float* sd, uint32_t* si) {
+        const int lane = lane_id();
+        if (valid && size == cap) {
+            const float wd = D()[size - 1];
+            const uint32_t wi = I()[size - 1] & VSG_ID_MASK;
+            valid = cand_less(cd, ci, wd, wi);
+        }
+        if (valid && maybe_dup) {
+            const int p = lower_bound(cd, ci);
+            if (p < size && D()[p] == cd && (I()[p] & VSG_ID_MASK) == ci) valid = false;
+        }
+        const uint64_t mask = __ballot(valid);
+        const int nc = popc64(mask);
+        if (nc == 0) return;
+        // rank among candidates
+        int rank = 0;
+        for (uint64_t m = mask; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            const float dj = readlane(cd, j);
+            const uint32_t ij = readlane(ci, j);
+            rank += cand_less(dj, ij, cd, ci) ? 1 : 0;
+        }
+        if (valid) {
+            sd[rank] = cd;
+            si[rank] = ci;
+        }
+        const int pos_new = valid ? rank + lower_bound(cd, ci) : 0;
+        wave_sync();
+        float* dd = D();
+        uint32_t* ii = I();
+        float* nd = Dn();
+        uint32_t* ni = In();
+        // existing entries shift by #candidates below them
+        for (int e = lane; e < size; e += 64) {
+            const float ed = dd[e];
+            const uint32_t ei = ii[e];
+            int lo = 0, hi = nc;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (cand_less(sd[mid], si[mid], ed, ei & VSG_ID_MASK)) lo = mid + 1;
+                else hi = mid;
+            }
+            const int p = e + lo;
+            if (p < cap) {
+                nd[p] = ed;
+                ni[p] = ei;
+            }
+        }
+        if (valid && pos_new < cap) {
+            nd[pos_new] = cd;
+            ni[pos_new] = ci;
+        }
+        size = min(size + nc, cap);
+        cur ^= 1;
+        wave_sync();
+    }
+};
+
+// ----------------------------------------------------------- graph access --
+
+struct GraphDev {
+    const uint8_t* vecs;
+    size_t row_bytes;
+    int nchunks;
+    uint32_t* adj0;
+    const uint32_t* upper_off;
+    uint32_t* upper;
+    int M, M0;
+
+    __device__ __forceinline__ uint32_t* row(uint32_t s, int l) const {
+        return l == 0 ? adj0 + (size_t)s * M0 : upper + ((size_t)upper_off[s] + (size_t)(l - 1)) * M;
+    }
+    __device__ __forceinline__ const uint8_t* vec(uint32_t s) const { return vecs + (size_t)s * row_bytes; }
+};
+
+}  // namespace vsg

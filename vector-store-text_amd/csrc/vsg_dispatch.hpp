@@ -1,0 +1,63 @@
+// vsg_dispatch.hpp — runtime (storage, metric, row shape) -> template instance.
+//
+// Row shape (G lanes per row, VM 16-B chunks per lane, U passes in flight)
+// is chosen from the row's 16-B chunk count so that a pass keeps 8-16 chunk
+// loads per lane outstanding:
+//   chunks <=   4: G 4,  VM 1,  U 4   (16 rows / pass)
+//   chunks <=  16: G 16, VM 1,  U 4
+//   chunks <=  32: G 32, VM 1,  U 8   (D=128 f32, D=256 f16)
+//   chunks <=  64: G 64, VM 1,  U 8
+//   chunks <= 128: G 64, VM 2,  U 4
+//   chunks <= 192: G 64, VM 3,  U 4   (D=768 f32)
+//   chunks <= 256: G 64, VM 4,  U 2
+//   chunks <= 384: G 64, VM 6,  U 2   (D=1536 f32)
+//   chunks <= 512: G 64, VM 8,  U 2
+//   chunks <=1024: G 64, VM 16, U 1
+#pragma once
+#include "vsg_device.hpp"
+#include "vsg_kernels.hpp"
+
+namespace vsg {
+
+template <int G_, int VM_, int U_> struct Shape {
+    static constexpr int G = G_, VM = VM_, U = U_;
+};
+template <typename T_> struct TypeTag {
+    using T = T_;
+};
+template <int M_> struct MetTag {
+    static constexpr int MET = M_;
+};
+
+template <typename F>
+inline void dispatch_shape(int nc, F&& f) {
+    if (nc <= 4) f(Shape<4, 1, 4>{});
+    else if (nc <= 16) f(Shape<16, 1, 4>{});
+    else if (nc <= 32) f(Shape<32, 1, 8>{});
+    else if (nc <= 64) f(Shape<64, 1, 8>{});
+    else if (nc <= 128) f(Shape<64, 2, 4>{});
+    else if (nc <= 192) f(Shape<64, 3, 4>{});
+    else if (nc <= 256) f(Shape<64, 4, 2>{});
+    else if (nc <= 384) f(Shape<64, 6, 2>{});
+    else if (nc <= 512) f(Shape<64, 8, 2>{});
+    else f(Shape<64, 16, 1>{});
+}
+
+// f(Shape, TypeTag, MetTag)
+template <typename F>
+inline void dispatch_all(Storage st, MetricKind mk, int nc, F&& f) {
+    dispatch_shape(nc, [&](auto sh) {
+        if (st == ST_F32) {
+            if (mk == MK_L2) f(sh, TypeTag<float>{}, MetTag<MET_L2>{});
+            else f(sh, TypeTag<float>{}, MetTag<MET_DOT>{});
+        } else {
+            if (mk == MK_L2) f(sh, TypeTag<_Float16>{}, MetTag<MET_L2>{});
+            else f(sh, TypeTag<_Float16>{}, MetTag<MET_DOT>{});
+        }
+    });
+}
+
+}  // namespace vsg
+
+#define VSG_KERNEL_OF(TEMPLATE, sh, tt, mt) \
+    TEMPLATE<decltype(sh)::G, decltype(sh)::VM, decltype(sh)::U, typename decltype(tt)::T, decltype(mt)::MET>

@@ -1,0 +1,811 @@
+// vsg_index.cpp — host side of libvsg: the C ABI (include/vsg.h) over the
+// gfx950 kernels.  Owns the HBM image of one index shard:
+//   vecs      slots x row_bytes   (f32 or f16, 16-B aligned rows, cos rows unit-normalised)
+//   adj0      slots x M0 u32      (level-0 adjacency, 0xFFFFFFFF padded, compact prefix)
+//   upper_off slots u32           (first upper row, or 0xFFFFFFFF)
+//   upper     rows x M u32        (row upper_off[s] + l - 1 = level l of slot s)
+//   keys      slots u64, flags slots u8 (bit 0 = tombstone)
+// and the host state the reference keeps around usearch (key map, entry point,
+// levels).  Reference call sites replaced: src/index/usearch.rs:98-309.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/vsg.h"
+#include "vsg_kernels.hpp"
+
+namespace vsg {
+hipError_t sort_pairs(void* temp, size_t& temp_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                      const uint32_t* vals_in, uint32_t* vals_out, size_t n, hipStream_t s);
+}
+
+using namespace vsg;
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e__ = (expr);                                                             \
+        if (e__ != hipSuccess)                                                               \
+            return fail(VSG_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e__));   \
+    } while (0)
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        hipGetDevice(&prev);
+        if (prev != dev) hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) hipSetDevice(prev);
+    }
+};
+
+template <typename X>
+hipError_t dev_alloc(X** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    return hipMalloc((void**)p, count * sizeof(X));
+}
+
+// level draw, bit-identical to oracle/vsg_oracle.c orc_sample_level
+uint64_t host_splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+int sample_level(uint64_t seed, uint64_t slot, uint32_t connectivity) {
+    uint64_t r = host_splitmix64(host_splitmix64(seed ^ 0x4C6576656C5EEDull) + slot);
+    double u = (double)((r >> 11) + 1) * (1.0 / 9007199254740992.0);
+    double lv = -log(u) / log((double)connectivity);
+    int l = (int)lv;
+    return l > 30 ? 30 : l;
+}
+
+double env_double(const char* name, double dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atof(v) : dflt;
+}
+
+}  // namespace
+
+struct vsg_index {
+    vsg_index_options_t opt{};
+    int dim = 0;
+    Storage st = ST_F32;
+    MetricKind mk = MK_L2;
+    bool normalize = false;
+    int M = 16, M0 = 32, efc = 128, ef = 64;
+    size_t elem = 4, row_bytes = 0;
+    int nchunks = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+
+    size_t cap = 0, slots = 0, live = 0;
+    uint8_t* d_vecs = nullptr;
+    uint32_t* d_adj0 = nullptr;
+    uint32_t* d_upper_off = nullptr;
+    uint32_t* d_upper = nullptr;
+    size_t upper_cap = 0, upper_used = 0;
+    uint64_t* d_keys = nullptr;
+    uint8_t* d_flags = nullptr;
+    unsigned long long* d_stats = nullptr;  // [0..2] search, [3..4] build
+
+    std::vector<int8_t> h_levels;
+    std::unordered_map<uint64_t, uint32_t> key2slot;
+    uint32_t entry = 0xFFFFFFFFu;
+    int max_level = -1;
+    std::atomic<uint64_t> build_vectors{0}, build_batches{0};
+
+    // build workspace (writer side only)
+    int8_t* d_blevels = nullptr;
+    uint32_t* d_pair_off = nullptr;
+    size_t bnodes_cap = 0;
+    uint64_t* d_pk[2] = {nullptr, nullptr};
+    uint32_t* d_pv[2] = {nullptr, nullptr};
+    size_t pairs_cap = 0;
+    void* d_sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    float* d_stage = nullptr;
+    size_t stage_cap = 0;  // rows
+
+    mutable std::shared_mutex mu;
+    int reverse_grid = 2048;
+
+    DevGraph graph() const {
+        DevGraph g;
+        g.vecs = d_vecs;
+        g.row_bytes = row_bytes;
+        g.nchunks = nchunks;
+        g.adj0 = d_adj0;
+        g.upper_off = d_upper_off;
+        g.upper = d_upper;
+        g.M = M;
+        g.M0 = M0;
+        return g;
+    }
+};
+
+static void free_dev(vsg_index* h) {
+    hipFree(h->d_vecs);
+    hipFree(h->d_adj0);
+    hipFree(h->d_upper_off);
+    hipFree(h->d_upper);
+    hipFree(h->d_keys);
+    hipFree(h->d_flags);
+    hipFree(h->d_stats);
+    hipFree(h->d_blevels);
+    hipFree(h->d_pair_off);
+    for (int i = 0; i < 2; ++i) {
+        hipFree(h->d_pk[i]);
+        hipFree(h->d_pv[i]);
+    }
+    hipFree(h->d_sort_tmp);
+    hipFree(h->d_stage);
+}
+
+// grow a device array, copying `used` elements and filling the tail with `fill`
+template <typename X>
+static int grow_array(X** arr, size_t used, size_t newcap, int fill, hipStream_t s) {
+    X* n = nullptr;
+    HIP_TRY(dev_alloc(&n, newcap));
+    if (used && *arr) HIP_TRY(hipMemcpyAsync(n, *arr, used * sizeof(X), hipMemcpyDeviceToDevice, s));
+    if (newcap > used) HIP_TRY(hipMemsetAsync(n + used, fill, (newcap - used) * sizeof(X), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    hipFree(*arr);
+    *arr = n;
+    return VSG_OK;
+}
+
+static int reserve_locked(vsg_index* h, size_t capacity) {
+    if (capacity <= h->cap) return VSG_OK;
+    if (capacity > MAX_SLOTS) return fail(VSG_EINVAL, "capacity exceeds 2^29 slots per shard");
+    const size_t s = h->slots;
+    uint8_t* nv = nullptr;
+    HIP_TRY(dev_alloc(&nv, capacity * h->row_bytes));
+    if (s) HIP_TRY(hipMemcpyAsync(nv, h->d_vecs, s * h->row_bytes, hipMemcpyDeviceToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    hipFree(h->d_vecs);
+    h->d_vecs = nv;
+    int rc;
+    if ((rc = grow_array(&h->d_adj0, s * h->M0, capacity * h->M0, 0xFF, h->stream))) return rc;
+    if ((rc = grow_array(&h->d_upper_off, s, capacity, 0xFF, h->stream))) return rc;
+    if ((rc = grow_array(&h->d_keys, s, capacity, 0xFF, h->stream))) return rc;
+    if ((rc = grow_array(&h->d_flags, s, capacity, 0, h->stream))) return rc;
+    h->h_levels.resize(capacity, 0);
+    h->cap = capacity;
+    return VSG_OK;
+}
+
+static int ensure_upper(vsg_index* h, size_t rows) {
+    if (rows <= h->upper_cap) return VSG_OK;
+    size_t want = std::max<size_t>(h->upper_cap * 2, 1024);
+    while (want < rows) want *= 2;
+    int rc = grow_array(&h->d_upper, h->upper_used * h->M, want * h->M, 0xFF, h->stream);
+    if (rc) return rc;
+    h->upper_cap = want;
+    return VSG_OK;
+}
+
+template <typename X>
+static int ensure_buf(X** p, size_t& cap, size_t need) {
+    if (need <= cap) return VSG_OK;
+    size_t want = std::max(need, cap * 2);
+    hipFree(*p);
+    *p = nullptr;
+    HIP_TRY(dev_alloc(p, want));
+    cap = want;
+    return VSG_OK;
+}
+
+// per-add node buffers (levels, pair offsets) and per-batch pair buffers
+static int ensure_nodes(vsg_index* h, size_t n) {
+    if (n <= h->bnodes_cap) return VSG_OK;
+    const size_t want = std::max(n, h->bnodes_cap * 2);
+    hipFree(h->d_blevels);
+    hipFree(h->d_pair_off);
+    h->d_blevels = nullptr;
+    h->d_pair_off = nullptr;
+    h->bnodes_cap = 0;
+    HIP_TRY(dev_alloc(&h->d_blevels, want));
+    HIP_TRY(dev_alloc(&h->d_pair_off, want));
+    h->bnodes_cap = want;
+    return VSG_OK;
+}
+
+static int ensure_pairs(vsg_index* h, size_t n) {
+    if (n <= h->pairs_cap) return VSG_OK;
+    const size_t want = std::max(n, h->pairs_cap * 2);
+    for (int i = 0; i < 2; ++i) {
+        hipFree(h->d_pk[i]);
+        hipFree(h->d_pv[i]);
+        h->d_pk[i] = nullptr;
+        h->d_pv[i] = nullptr;
+    }
+    h->pairs_cap = 0;
+    for (int i = 0; i < 2; ++i) {
+        HIP_TRY(dev_alloc(&h->d_pk[i], want));
+        HIP_TRY(dev_alloc(&h->d_pv[i], want));
+    }
+    h->pairs_cap = want;
+    return VSG_OK;
+}
+
+// Validates keys (no reserved key, no live duplicate, none inside the batch).
+static int check_keys(vsg_index* h, const uint64_t* keys, size_t n) {
+    std::unordered_set<uint64_t> seen;
+    seen.reserve(n * 2);
+    for (size_t i = 0; i < n; ++i) {
+        if (keys[i] == VSG_NO_KEY) return fail(VSG_EINVAL, "key UINT64_MAX is reserved");
+        if (h->key2slot.count(keys[i])) return fail(VSG_EDUPKEY, "Duplicate keys not allowed: " + std::to_string(keys[i]));
+        if (!seen.insert(keys[i]).second) return fail(VSG_EDUPKEY, "Duplicate key inside batch: " + std::to_string(keys[i]));
+    }
+    return VSG_OK;
+}
+
+// Batched HNSW insertion of slots [s0, s0 + n) whose rows are already in d_vecs.
+static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* keys) {
+    hipStream_t st = h->stream;
+    // levels and upper rows
+    std::vector<uint32_t> upper_off(n);
+    size_t need_upper = h->upper_used;
+    for (size_t i = 0; i < n; ++i) {
+        const int L = sample_level(h->opt.seed, s0 + i, (uint32_t)h->M);
+        h->h_levels[s0 + i] = (int8_t)L;
+        upper_off[i] = L > 0 ? (uint32_t)need_upper : 0xFFFFFFFFu;
+        need_upper += (size_t)L;
+    }
+    int rc = ensure_upper(h, need_upper);
+    if (rc) return rc;
+    h->upper_used = need_upper;
+    HIP_TRY(hipMemcpyAsync(h->d_upper_off + s0, upper_off.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_keys + s0, keys, n * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(h->d_flags + s0, 0, n, st));
+    for (size_t i = 0; i < n; ++i) h->key2slot[keys[i]] = s0 + (uint32_t)i;
+    h->slots += n;
+    h->live += n;
+
+    if ((rc = ensure_nodes(h, n))) return rc;
+    HIP_TRY(hipMemcpyAsync(h->d_blevels, h->h_levels.data() + s0, n, hipMemcpyHostToDevice, st));
+
+    const double frac = env_double("VSG_BUILD_BATCH_FRAC", 1.0 / 16.0);
+    const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 32768);
+    std::vector<uint32_t> pair_off(n + 1);
+
+    size_t i = 0;
+    if (h->entry == 0xFFFFFFFFu) {
+        h->entry = s0;
+        h->max_level = h->h_levels[s0];
+        i = 1;
+    }
+    while (i < n) {
+        const size_t graph_nodes = (size_t)s0 + i;
+        size_t b = (size_t)std::floor((double)graph_nodes * frac);
+        b = std::max<size_t>(1, std::min(b, bmax));
+        b = std::min(b, n - i);
+        int new_top = -1;
+        for (size_t j = i; j < i + b; ++j) {
+            if (h->h_levels[s0 + j] > h->max_level) {
+                b = j - i + 1;
+                new_top = h->h_levels[s0 + j];
+                break;
+            }
+        }
+        // pair offsets: each node emits <= M0 + min(L, maxl) * M pairs
+        uint32_t acc = 0;
+        for (size_t j = 0; j < b; ++j) {
+            pair_off[i + j] = acc;
+            const int L = std::min<int>(h->h_levels[s0 + i + j], h->max_level);
+            acc += (uint32_t)(h->M0 + L * h->M);
+        }
+        const size_t npairs = acc;
+        if ((rc = ensure_pairs(h, npairs))) return rc;
+        HIP_TRY(hipMemcpyAsync(h->d_pair_off + i, pair_off.data() + i, b * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemsetAsync(h->d_pk[0], 0xFF, npairs * 8, st));
+
+        InsertParams ip{};
+        ip.g = h->graph();
+        ip.base_slot = s0 + (uint32_t)i;
+        ip.nnodes = (int)b;
+        ip.levels = h->d_blevels + i;
+        ip.pair_off = h->d_pair_off + i;
+        ip.pair_keys = h->d_pk[0];
+        ip.pair_vals = h->d_pv[0];
+        ip.entry = h->entry;
+        ip.max_level = h->max_level;
+        ip.efc = h->efc;
+        ip.stats = h->d_stats;
+        HIP_TRY(launch_insert(h->st, h->mk, ip, st));
+
+        size_t tmp = 0;
+        HIP_TRY(sort_pairs(nullptr, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], npairs, st));
+        if (tmp > h->sort_tmp_bytes) {
+            hipFree(h->d_sort_tmp);
+            h->d_sort_tmp = nullptr;
+            HIP_TRY(hipMalloc(&h->d_sort_tmp, tmp * 2));
+            h->sort_tmp_bytes = tmp * 2;
+        }
+        tmp = h->sort_tmp_bytes;
+        HIP_TRY(sort_pairs(h->d_sort_tmp, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], npairs, st));
+
+        ReverseParams rp{};
+        rp.g = h->graph();
+        rp.keys = h->d_pk[1];
+        rp.vals = h->d_pv[1];
+        rp.npairs = npairs;
+        rp.stats = h->d_stats;
+        const int grid = (int)std::max<size_t>(1, std::min<size_t>((size_t)h->reverse_grid, (npairs + 63) / 64));
+        HIP_TRY(launch_reverse(h->st, h->mk, rp, grid, st));
+
+        if (new_top >= 0) {
+            h->entry = s0 + (uint32_t)(i + b - 1);
+            h->max_level = new_top;
+        }
+        h->build_batches++;
+        i += b;
+    }
+    h->build_vectors += n;
+    return VSG_OK;
+}
+
+// ----------------------------------------------------------------- C ABI --
+
+extern "C" {
+
+const char* vsg_last_error(void) { return g_last_error.c_str(); }
+const char* vsg_version(void) { return "vsg 0.1.0 gfx950"; }
+
+int vsg_sample_level(uint64_t seed, uint64_t slot, uint32_t connectivity) {
+    return sample_level(seed, slot, connectivity);
+}
+
+int vsg_index_new(const vsg_index_options_t* o, vsg_index_t** out) {
+    if (!o || !out) return fail(VSG_EINVAL, "null argument");
+    *out = nullptr;
+    if (o->dimensions == 0) return fail(VSG_EINVAL, "dimensions == 0");
+    if (o->metric > VSG_METRIC_COS) return fail(VSG_EINVAL, "unknown metric");
+    if (o->quantization > VSG_SCALAR_F16) return fail(VSG_EINVAL, "unknown quantization");
+    const uint32_t M = o->connectivity ? o->connectivity : 16;
+    if (M < 2 || M > 32) return fail(VSG_EUNSUPPORTED, "connectivity must be in [2, 32]");
+    auto* h = new vsg_index();
+    h->opt = *o;
+    h->dim = (int)o->dimensions;
+    h->st = o->quantization == VSG_SCALAR_F16 ? ST_F16 : ST_F32;
+    h->mk = o->metric == VSG_METRIC_L2SQ ? MK_L2 : MK_DOT;
+    h->normalize = o->metric == VSG_METRIC_COS;
+    h->M = (int)M;
+    h->M0 = 2 * (int)M;
+    h->efc = o->expansion_add ? (int)o->expansion_add : 128;
+    h->ef = o->expansion_search ? (int)o->expansion_search : 64;
+    if (h->efc > 1024) h->efc = 1024;
+    h->elem = h->st == ST_F16 ? 2 : 4;
+    const size_t per_chunk = 16 / h->elem;
+    const size_t padded = (h->dim + per_chunk - 1) / per_chunk * per_chunk;
+    h->row_bytes = padded * h->elem;
+    h->nchunks = (int)(h->row_bytes / 16);
+    if (!shape_supported(h->nchunks)) {
+        delete h;
+        return fail(VSG_EUNSUPPORTED, "dimensions too large (max 4096 f32 / 8192 f16)");
+    }
+    h->device = o->device;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        delete h;
+        return fail(VSG_EDEVICE, "no HIP device visible");
+    }
+    if (h->device < 0 || h->device >= ndev) {
+        delete h;
+        return fail(VSG_EINVAL, "device ordinal out of range");
+    }
+    DeviceGuard dg(h->device);
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail(VSG_EDEVICE, "hipStreamCreate failed");
+    }
+    if (hipMalloc(&h->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        delete h;
+        return fail(VSG_ENOMEM, "stats allocation failed");
+    }
+    *out = h;
+    return VSG_OK;
+}
+
+void vsg_index_free(vsg_index_t* h) {
+    if (!h) return;
+    {
+        DeviceGuard dg(h->device);
+        hipStreamSynchronize(h->stream);
+        free_dev(h);
+        hipStreamDestroy(h->stream);
+    }
+    delete h;
+}
+
+int vsg_index_reserve(vsg_index_t* h, size_t capacity) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    return reserve_locked(h, capacity);
+}
+
+size_t vsg_index_capacity(const vsg_index_t* h) { return h ? h->cap : 0; }
+size_t vsg_index_size(const vsg_index_t* h) {
+    if (!h) return 0;
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    return h->live;
+}
+size_t vsg_index_dimensions(const vsg_index_t* h) { return h ? (size_t)h->dim : 0; }
+int vsg_index_contains(const vsg_index_t* h, uint64_t key) {
+    if (!h) return 0;
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    return h->key2slot.count(key) ? 1 : 0;
+}
+
+static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, size_t n, bool device_src,
+                      hipStream_t user_stream) {
+    if (!h || (!keys && n) || (!vecs && n)) return fail(VSG_EINVAL, "null argument");
+    if (n == 0) return VSG_OK;
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    int rc = check_keys(h, keys, n);
+    if (rc) return rc;
+    if (h->slots + n > MAX_SLOTS) return fail(VSG_EINVAL, "index full (2^29 slots per shard)");
+    if (h->slots + n > h->cap) {
+        size_t want = std::max<size_t>(h->cap * 2, 1024);
+        while (want < h->slots + n) want *= 2;
+        if ((rc = reserve_locked(h, std::min<size_t>(want, MAX_SLOTS)))) return rc;
+    }
+    const uint32_t s0 = (uint32_t)h->slots;
+    if (device_src) {
+        // order after the producer of `vecs` on the caller's stream (NULL = default stream)
+        hipEvent_t ev;
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ev, user_stream));
+        HIP_TRY(hipStreamWaitEvent(h->stream, ev, 0));
+        HIP_TRY(hipEventDestroy(ev));
+        HIP_TRY(launch_prepare(h->st, vecs, n, h->dim, h->normalize, h->d_vecs + (size_t)s0 * h->row_bytes,
+                               h->row_bytes, h->stream));
+    } else {
+        const size_t chunk = 65536;
+        if ((rc = ensure_buf(&h->d_stage, h->stage_cap, std::min(n, chunk) * h->dim))) return rc;
+        for (size_t off = 0; off < n; off += chunk) {
+            const size_t c = std::min(chunk, n - off);
+            HIP_TRY(hipMemcpyAsync(h->d_stage, vecs + off * h->dim, c * h->dim * 4, hipMemcpyHostToDevice, h->stream));
+            HIP_TRY(launch_prepare(h->st, h->d_stage, c, h->dim, h->normalize,
+                                   h->d_vecs + (size_t)(s0 + off) * h->row_bytes, h->row_bytes, h->stream));
+            HIP_TRY(hipStreamSynchronize(h->stream));
+        }
+    }
+    rc = insert_slots(h, s0, n, keys);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return VSG_OK;
+}
+
+int vsg_index_add(vsg_index_t* h, const uint64_t* keys, const float* vectors, size_t n) {
+    return add_common(h, keys, vectors, n, false, nullptr);
+}
+
+int vsg_index_add_device(vsg_index_t* h, const uint64_t* keys, const float* vectors_device, size_t n,
+                         void* stream) {
+    return add_common(h, keys, vectors_device, n, true, (hipStream_t)stream);
+}
+
+int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_removed) {
+    if (!h || (!keys && n)) return fail(VSG_EINVAL, "null argument");
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    std::vector<uint32_t> slots;
+    for (size_t i = 0; i < n; ++i) {
+        auto it = h->key2slot.find(keys[i]);
+        if (it == h->key2slot.end()) continue;
+        slots.push_back(it->second);
+        h->key2slot.erase(it);
+    }
+    if (!slots.empty()) {
+        uint32_t* d = nullptr;
+        HIP_TRY(hipMallocAsync((void**)&d, slots.size() * 4, h->stream));
+        HIP_TRY(hipMemcpyAsync(d, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(launch_set_flags(h->d_flags, d, slots.size(), 1, h->stream));
+        HIP_TRY(hipFreeAsync(d, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    h->live -= slots.size();
+    if (n_removed) *n_removed = slots.size();
+    return VSG_OK;
+}
+
+static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, size_t k, size_t ef,
+                                uint64_t* ok, float* od, uint32_t* oc, hipStream_t s, bool exact) {
+    if (k == 0) return fail(VSG_EINVAL, "k must be >= 1 (Limit is NonZeroUsize)");
+    if (nq == 0) return VSG_OK;
+    if (k > 1024) return fail(VSG_EUNSUPPORTED, "k > 1024");
+    uint8_t* qp = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&qp, nq * h->row_bytes, s));
+    HIP_TRY(launch_prepare(h->st, q_dev, nq, h->dim, h->normalize, qp, h->row_bytes, s));
+    if (!exact) {
+        size_t e = ef ? ef : (size_t)h->ef;
+        e = std::max(e, k);
+        if (e > 1024) e = 1024;
+        SearchParams p{};
+        p.g = h->graph();
+        p.queries = qp;
+        p.nq = (int)nq;
+        p.k = (int)k;
+        p.ef = (int)e;
+        p.entry = h->entry;
+        p.max_level = h->max_level;
+        p.flags = h->d_flags;
+        p.keys = h->d_keys;
+        p.out_keys = ok;
+        p.out_dist = od;
+        p.out_counts = oc;
+        p.stats = h->d_stats;
+        HIP_TRY(launch_search(h->st, h->mk, p, s));
+    } else {
+        const size_t slots = h->slots;
+        int nblocks = (int)std::max<size_t>(1, (slots + 4095) / 4096);
+        const int rpb = (int)((slots + nblocks - 1) / nblocks);
+        if (slots == 0) nblocks = 1;
+        float* pd = nullptr;
+        uint32_t* pi = nullptr;
+        const size_t np = nq * (size_t)nblocks * k;
+        HIP_TRY(hipMallocAsync((void**)&pd, np * 4, s));
+        HIP_TRY(hipMallocAsync((void**)&pi, np * 4, s));
+        ExactParams ep{};
+        ep.vecs = h->d_vecs;
+        ep.row_bytes = h->row_bytes;
+        ep.nchunks = h->nchunks;
+        ep.queries = qp;
+        ep.nq = (int)nq;
+        ep.k = (int)k;
+        ep.nslots = slots;
+        ep.rows_per_block = std::max(rpb, 1);
+        ep.nblocks = nblocks;
+        ep.flags = h->d_flags;
+        ep.part_d = pd;
+        ep.part_i = pi;
+        if (slots > 0) {
+            HIP_TRY(launch_exact(h->st, h->mk, ep, s));
+        } else {
+            HIP_TRY(hipMemsetAsync(pi, 0xFF, np * 4, s));
+        }
+        MergeParams mp{};
+        mp.part_d = pd;
+        mp.part_i = pi;
+        mp.nq = (int)nq;
+        mp.parts = nblocks;
+        mp.k = (int)k;
+        mp.keys = h->d_keys;
+        mp.out_keys = ok;
+        mp.out_dist = od;
+        mp.out_counts = oc;
+        HIP_TRY(launch_merge_parts(mp, s));
+        HIP_TRY(hipFreeAsync(pd, s));
+        HIP_TRY(hipFreeAsync(pi, s));
+    }
+    HIP_TRY(hipFreeAsync(qp, s));
+    return VSG_OK;
+}
+
+static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
+                       float* out_dist, size_t* out_counts, bool exact) {
+    if (!h || (!queries && nq) || (!out_keys && nq) || (!out_dist && nq)) return fail(VSG_EINVAL, "null argument");
+    if (k == 0) return fail(VSG_EINVAL, "k must be >= 1 (Limit is NonZeroUsize)");
+    if (nq == 0) return VSG_OK;
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    hipStream_t s;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    float* dq = nullptr;
+    uint64_t* dk = nullptr;
+    float* dd = nullptr;
+    uint32_t* dc = nullptr;
+    int rc = VSG_OK;
+    std::vector<uint32_t> counts(nq);
+    do {
+        if (hipMallocAsync((void**)&dq, nq * h->dim * 4, s) != hipSuccess ||
+            hipMallocAsync((void**)&dk, nq * k * 8, s) != hipSuccess ||
+            hipMallocAsync((void**)&dd, nq * k * 4, s) != hipSuccess ||
+            hipMallocAsync((void**)&dc, nq * 4, s) != hipSuccess) {
+            rc = fail(VSG_ENOMEM, "search workspace");
+            break;
+        }
+        if (hipMemcpyAsync(dq, queries, nq * h->dim * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
+            rc = fail(VSG_EDEVICE, "H2D queries");
+            break;
+        }
+        rc = search_device_locked(h, dq, nq, k, ef, dk, dd, dc, s, exact);
+        if (rc) break;
+        if (hipMemcpyAsync(out_keys, dk, nq * k * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(out_dist, dd, nq * k * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(counts.data(), dc, nq * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
+            rc = fail(VSG_EDEVICE, "D2H results");
+            break;
+        }
+    } while (0);
+    if (dq) hipFreeAsync(dq, s);
+    if (dk) hipFreeAsync(dk, s);
+    if (dd) hipFreeAsync(dd, s);
+    if (dc) hipFreeAsync(dc, s);
+    hipError_t e = hipStreamSynchronize(s);
+    hipStreamDestroy(s);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(VSG_EDEVICE, std::string("search: ") + hipGetErrorString(e));
+    if (out_counts)
+        for (size_t i = 0; i < nq; ++i) out_counts[i] = counts[i];
+    return VSG_OK;
+}
+
+int vsg_index_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
+                     float* out_distances, size_t* out_counts) {
+    return search_host(h, queries, nq, k, ef, out_keys, out_distances, out_counts, false);
+}
+
+int vsg_index_exact_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, uint64_t* out_keys,
+                           float* out_distances, size_t* out_counts) {
+    return search_host(h, queries, nq, k, 0, out_keys, out_distances, out_counts, true);
+}
+
+int vsg_index_search_device(vsg_index_t* h, const float* q, size_t nq, size_t k, size_t ef, uint64_t* ok,
+                            float* od, uint32_t* oc, void* stream) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    return search_device_locked(h, q, nq, k, ef, ok, od, oc, (hipStream_t)stream, false);
+}
+
+int vsg_index_exact_search_device(vsg_index_t* h, const float* q, size_t nq, size_t k, uint64_t* ok, float* od,
+                                  uint32_t* oc, void* stream) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    return search_device_locked(h, q, nq, k, 0, ok, od, oc, (hipStream_t)stream, true);
+}
+
+int vsg_merge_topk_device(const uint64_t* keys, const float* dist, size_t parts, size_t nq, size_t k,
+                          uint64_t* out_keys, float* out_dist, void* stream) {
+    if (parts == 0 || parts > 64) return fail(VSG_EINVAL, "parts must be in [1, 64]");
+    HIP_TRY(launch_merge_topk64(keys, dist, (int)parts, (int)nq, (int)k, out_keys, out_dist, (hipStream_t)stream));
+    return VSG_OK;
+}
+
+int vsg_index_stats(const vsg_index_t* h, vsg_stats_t* out) {
+    if (!h || !out) return fail(VSG_EINVAL, "null argument");
+    DeviceGuard dg(h->device);
+    unsigned long long s[16];
+    HIP_TRY(hipMemcpy(s, h->d_stats, sizeof(s), hipMemcpyDeviceToHost));
+    out->search_distances = s[0];
+    out->search_adjacency = s[1];
+    out->search_queries = s[2];
+    out->build_distances = s[3];
+    out->build_adjacency = s[4];
+    out->build_vectors = h->build_vectors.load();
+    out->build_batches = h->build_batches.load();
+    return VSG_OK;
+}
+
+int vsg_index_reset_stats(vsg_index_t* h) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    DeviceGuard dg(h->device);
+    HIP_TRY(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
+    h->build_vectors = 0;
+    h->build_batches = 0;
+    return VSG_OK;
+}
+
+int vsg_index_graph_info(const vsg_index_t* h, size_t* slots, size_t* upper_rows, size_t* connectivity,
+                         uint32_t* entry, int* max_level) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    if (slots) *slots = h->slots;
+    if (upper_rows) *upper_rows = h->upper_used;
+    if (connectivity) *connectivity = (size_t)h->M;
+    if (entry) *entry = h->entry;
+    if (max_level) *max_level = h->max_level;
+    return VSG_OK;
+}
+
+int vsg_index_export(const vsg_index_t* h, float* vectors, uint64_t* keys, uint8_t* removed, int8_t* levels,
+                     uint32_t* adj0, uint32_t* upper_off, uint32_t* upper) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    const size_t s = h->slots;
+    hipStream_t st = h->stream;
+    if (vectors && s) {
+        float* d = nullptr;
+        HIP_TRY(hipMalloc(&d, s * h->dim * 4));
+        HIP_TRY(launch_unprepare(h->st, h->d_vecs, s, h->dim, h->row_bytes, d, st));
+        HIP_TRY(hipMemcpyAsync(vectors, d, s * h->dim * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        hipFree(d);
+    }
+    if (keys && s) HIP_TRY(hipMemcpyAsync(keys, h->d_keys, s * 8, hipMemcpyDeviceToHost, st));
+    if (removed && s) HIP_TRY(hipMemcpyAsync(removed, h->d_flags, s, hipMemcpyDeviceToHost, st));
+    if (levels && s) memcpy(levels, h->h_levels.data(), s);
+    if (adj0 && s) HIP_TRY(hipMemcpyAsync(adj0, h->d_adj0, s * h->M0 * 4, hipMemcpyDeviceToHost, st));
+    if (upper_off && s) HIP_TRY(hipMemcpyAsync(upper_off, h->d_upper_off, s * 4, hipMemcpyDeviceToHost, st));
+    if (upper && h->upper_used)
+        HIP_TRY(hipMemcpyAsync(upper, h->d_upper, h->upper_used * h->M * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (removed)
+        for (size_t i = 0; i < s; ++i) removed[i] &= 1;
+    return VSG_OK;
+}
+
+int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const uint64_t* keys,
+                     const uint8_t* removed, const int8_t* levels, const uint32_t* adj0, const uint32_t* upper_off,
+                     const uint32_t* upper, size_t upper_rows, uint32_t entry, int max_level) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    if (h->slots) return fail(VSG_EINVAL, "import requires an empty index");
+    if (slots == 0) return VSG_OK;
+    int rc = reserve_locked(h, slots);
+    if (rc) return rc;
+    if ((rc = ensure_upper(h, upper_rows))) return rc;
+    hipStream_t st = h->stream;
+    float* d = nullptr;
+    HIP_TRY(hipMalloc(&d, slots * h->dim * 4));
+    HIP_TRY(hipMemcpyAsync(d, vectors, slots * h->dim * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_prepare(h->st, d, slots, h->dim, h->normalize, h->d_vecs, h->row_bytes, st));
+    HIP_TRY(hipMemcpyAsync(h->d_keys, keys, slots * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_flags, removed, slots, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_adj0, adj0, slots * h->M0 * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_upper_off, upper_off, slots * 4, hipMemcpyHostToDevice, st));
+    if (upper_rows) HIP_TRY(hipMemcpyAsync(h->d_upper, upper, upper_rows * h->M * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    hipFree(d);
+    memcpy(h->h_levels.data(), levels, slots);
+    h->upper_used = upper_rows;
+    h->slots = slots;
+    h->live = 0;
+    for (size_t i = 0; i < slots; ++i)
+        if (!(removed[i] & 1)) {
+            h->key2slot[keys[i]] = (uint32_t)i;
+            h->live++;
+        }
+    h->entry = entry;
+    h->max_level = max_level;
+    return VSG_OK;
+}
+
+int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed, size_t start_row,
+                       float* out, void* stream) {
+    if (kind < 0 || kind > 2 || dim == 0) return fail(VSG_EINVAL, "bad datagen arguments");
+    hipStream_t s = (hipStream_t)stream;
+    float *w = nullptr, *c = nullptr;
+    if (kind == 0) {
+        HIP_TRY(hipMallocAsync((void**)&w, 64 * dim * 4, s));
+        HIP_TRY(hipMallocAsync((void**)&c, 1024 * 64 * 4, s));
+    }
+    HIP_TRY(launch_datagen(kind, n, dim, seed, model_seed, start_row, out, w, c, s));
+    if (w) HIP_TRY(hipFreeAsync(w, s));
+    if (c) HIP_TRY(hipFreeAsync(c, s));
+    return VSG_OK;
+}
+
+}  // extern "C"

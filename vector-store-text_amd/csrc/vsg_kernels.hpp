@@ -1,0 +1,112 @@
+// vsg_kernels.hpp — host-side launch interface of the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace vsg {
+
+enum Storage { ST_F32 = 0, ST_F16 = 1 };
+enum MetricKind { MK_L2 = 0, MK_DOT = 1 };  // cos = DOT on normalised rows
+
+struct DevGraph {
+    const uint8_t* vecs;
+    size_t row_bytes;
+    int nchunks;
+    uint32_t* adj0;
+    const uint32_t* upper_off;
+    uint32_t* upper;
+    int M, M0;
+};
+
+struct SearchParams {
+    DevGraph g;
+    const uint8_t* queries;  // prepared rows, g.row_bytes stride
+    int nq, k, ef;
+    uint32_t entry;
+    int max_level;
+    const uint8_t* flags;
+    const uint64_t* keys;
+    uint64_t* out_keys;
+    float* out_dist;
+    uint32_t* out_counts;
+    unsigned long long* stats;  // [0] n_dist, [1] n_adj, [2] queries
+};
+
+struct InsertParams {
+    DevGraph g;
+    uint32_t base_slot;
+    int nnodes;
+    const int8_t* levels;      // per batch node
+    const uint32_t* pair_off;  // per batch node
+    uint64_t* pair_keys;
+    uint32_t* pair_vals;
+    uint32_t entry;
+    int max_level;
+    int efc;
+    unsigned long long* stats;  // [3] n_dist, [4] n_adj
+};
+
+struct ReverseParams {
+    DevGraph g;
+    const uint64_t* keys;  // sorted (level:5 | v:29 | u:29 | pad)
+    const uint32_t* vals;  // f32 bits: dist(u, v)
+    size_t npairs;
+    unsigned long long* stats;
+};
+
+struct ExactParams {
+    const uint8_t* vecs;
+    size_t row_bytes;
+    int nchunks;
+    const uint8_t* queries;
+    int nq, k;
+    size_t nslots;
+    int rows_per_block;
+    int nblocks;
+    const uint8_t* flags;
+    float* part_d;     // nq x nblocks x k
+    uint32_t* part_i;  // nq x nblocks x k
+};
+
+struct MergeParams {
+    const float* part_d;
+    const uint32_t* part_i;
+    int nq, parts, k;
+    const uint64_t* keys;  // slot -> key (NULL: ids are already keys, 64-bit inputs)
+    uint64_t* out_keys;
+    float* out_dist;
+    uint32_t* out_counts;
+};
+
+// key layout of the reverse-link pairs
+constexpr int PAIR_U_BITS = 29;
+constexpr int PAIR_V_SHIFT = 29;
+constexpr int PAIR_L_SHIFT = 58;
+constexpr uint64_t PAIR_ID_MASK = (1ull << 29) - 1;
+constexpr uint32_t MAX_SLOTS = 1u << 29;
+
+bool shape_supported(int nchunks);
+size_t search_lds_bytes(int ef);
+size_t insert_lds_bytes(int efc);
+
+hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
+hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s);
+hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s);
+hipError_t launch_exact(Storage st, MetricKind mk, const ExactParams& p, hipStream_t s);
+hipError_t launch_merge_parts(const MergeParams& p, hipStream_t s);
+hipError_t launch_merge_topk64(const uint64_t* keys, const float* dist, int parts, int nq, int k,
+                               uint64_t* out_keys, float* out_dist, hipStream_t s);
+// f32 rows (stride dim) -> storage rows (row_bytes), normalised when `normalize`
+hipError_t launch_prepare(Storage st, const float* in, size_t n, int dim, bool normalize,
+                          uint8_t* out, size_t row_bytes, hipStream_t s);
+// storage rows -> f32 rows (stride dim)
+hipError_t launch_unprepare(Storage st, const uint8_t* in, size_t n, int dim, size_t row_bytes,
+                            float* out, hipStream_t s);
+hipError_t launch_set_flags(uint8_t* flags, const uint32_t* slots, size_t n, uint8_t value,
+                            hipStream_t s);
+hipError_t launch_datagen(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed,
+                          size_t start_row, float* out, float* scratch_w, float* scratch_c,
+                          hipStream_t s);
+
+}  // namespace vsg

@@ -1,0 +1,125 @@
+"""ctypes binding of libvsg.so (include/vsg.h).
+
+The product path: every call goes to the gfx950 HIP library.  There is no CPU
+fallback — if the shared library is missing or no GPU is visible, calls fail
+loudly (the oracle under /root/repo/oracle is test infrastructure only).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libvsg.so")
+HEADER = os.path.join(REPO_ROOT, "include", "vsg.h")
+
+VSG_OK = 0
+VSG_EINVAL = 1
+VSG_ENOMEM = 2
+VSG_EDUPKEY = 3
+VSG_EDEVICE = 4
+VSG_EUNSUPPORTED = 5
+
+METRICS = {"l2sq": 0, "ip": 1, "cos": 2}
+SCALARS = {"f32": 0, "f16": 1}
+NO_KEY = (1 << 64) - 1
+
+
+class VsgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"vsg error {code}: {msg}")
+        self.code = code
+
+
+class DuplicateKeyError(VsgError, KeyError):
+    pass
+
+
+class Options(C.Structure):
+    _fields_ = [
+        ("dimensions", C.c_uint32),
+        ("metric", C.c_uint32),
+        ("quantization", C.c_uint32),
+        ("connectivity", C.c_uint32),
+        ("expansion_add", C.c_uint32),
+        ("expansion_search", C.c_uint32),
+        ("device", C.c_int32),
+        ("flags", C.c_uint32),
+        ("seed", C.c_uint64),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("search_queries", C.c_uint64),
+        ("search_distances", C.c_uint64),
+        ("search_adjacency", C.c_uint64),
+        ("build_vectors", C.c_uint64),
+        ("build_distances", C.c_uint64),
+        ("build_adjacency", C.c_uint64),
+        ("build_batches", C.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def declared_symbols() -> list[str]:
+    """Every function declared in include/vsg.h."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(vsg_\w+)\s*\(", txt, re.M)))
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libvsg.so not built at {LIB_PATH}: run `make -C vector-store-text_amd` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    P, sz, u64, u32 = C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint32
+    sigs = {
+        "vsg_index_new": (C.c_int, [C.POINTER(Options), C.POINTER(P)]),
+        "vsg_index_free": (None, [P]),
+        "vsg_index_reserve": (C.c_int, [P, sz]),
+        "vsg_index_capacity": (sz, [P]),
+        "vsg_index_size": (sz, [P]),
+        "vsg_index_dimensions": (sz, [P]),
+        "vsg_index_contains": (C.c_int, [P, u64]),
+        "vsg_index_add": (C.c_int, [P, P, P, sz]),
+        "vsg_index_add_device": (C.c_int, [P, P, P, sz, P]),
+        "vsg_index_remove": (C.c_int, [P, P, sz, C.POINTER(sz)]),
+        "vsg_index_search": (C.c_int, [P, P, sz, sz, sz, P, P, P]),
+        "vsg_index_exact_search": (C.c_int, [P, P, sz, sz, P, P, P]),
+        "vsg_index_search_device": (C.c_int, [P, P, sz, sz, sz, P, P, P, P]),
+        "vsg_index_exact_search_device": (C.c_int, [P, P, sz, sz, P, P, P, P]),
+        "vsg_merge_topk_device": (C.c_int, [P, P, sz, sz, sz, P, P, P]),
+        "vsg_index_stats": (C.c_int, [P, C.POINTER(Stats)]),
+        "vsg_index_reset_stats": (C.c_int, [P]),
+        "vsg_index_graph_info": (C.c_int, [P, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz),
+                                           C.POINTER(u32), C.POINTER(C.c_int)]),
+        "vsg_index_export": (C.c_int, [P] * 8),
+        "vsg_index_import": (C.c_int, [P, sz, P, P, P, P, P, P, P, sz, u32, C.c_int]),
+        "vsg_datagen_device": (C.c_int, [C.c_int, sz, sz, u64, u64, sz, P, P]),
+        "vsg_sample_level": (C.c_int, [u64, u64, u32]),
+        "vsg_last_error": (C.c_char_p, []),
+        "vsg_version": (C.c_char_p, []),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc == VSG_OK:
+        return
+    msg = lib().vsg_last_error().decode(errors="replace")
+    if rc == VSG_EDUPKEY:
+        raise DuplicateKeyError(rc, msg)
+    raise VsgError(rc, msg)

@@ -209,12 +209,32 @@ def main():
         dist.destroy_process_group()
 
 
+def host_cores() -> int:
+    """SCYLLA_USEARCH_BACKGROUND_THREADS (README.md:14-15), else this process's
+    real CPU share: cgroup cpu.max quota, then affinity (os.cpu_count() reports
+    the whole machine on the GPU box, not our share)."""
+    env = int(os.environ.get("SCYLLA_USEARCH_BACKGROUND_THREADS", "0") or 0)
+    if env > 0:
+        return env
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        n = min(n, omp)
+    return max(1, n)
+
+
 def cpu_baseline(a, index, q_t, ef, x_t):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # the checker / CPU baseline only (never the product path)
 
     O.set_fast_metric(True)
-    threads = int(os.environ.get("SCYLLA_USEARCH_BACKGROUND_THREADS", "0")) or os.cpu_count()
+    threads = host_cores()
     res = {"unit": "queries/s", "cores": threads, "kind": "port"}
     # (1) search QPS: the same graph, exported from HBM, searched by the C restatement
     g = index.export()

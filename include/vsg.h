@@ -150,7 +150,8 @@ int vsg_index_import(vsg_index_t* index, size_t slots, const float* vectors,
                      size_t upper_rows, uint32_t entry, int max_level);
 
 /* Synthetic inputs generated in HBM (vsg/datagen.py formulas): kind 0 =
- * clustered-latent, 1 = iid gaussian, 2 = uint8-valued. */
+ * clustered-latent, 1 = iid gaussian, 2 = uint8-valued, 3 = SIFT-like
+ * (clustered, ReLU, x48, rounded into 0..255). */
 int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed,
                        size_t start_row, float* out_device, void* stream);
 

@@ -354,6 +354,9 @@ struct orc_hnsw {
     pthread_mutex_t* node_locks;
     pthread_mutex_t global_lock;
     keymap km;
+    void* sscr; /* cached search scratch (scratch_t[sscr_n]) */
+    int sscr_n;
+    size_t sscr_slots, sscr_ef;
 };
 
 static inline const float* VEC(const orc_hnsw* h, uint32_t s) { return h->vecs + (size_t)s * h->dim; }
@@ -386,8 +389,11 @@ orc_hnsw* orc_hnsw_new(size_t dim, int metric, size_t connectivity, size_t expan
     return h;
 }
 
+static void free_search_scratch(orc_hnsw* h);
+
 void orc_hnsw_free(orc_hnsw* h) {
     if (!h) return;
+    free_search_scratch(h);
     if (h->node_locks)
         for (size_t i = 0; i < h->cap; ++i) pthread_mutex_destroy(&h->node_locks[i]);
     free(h->node_locks);
@@ -471,6 +477,14 @@ static void scratch_free(scratch_t* s) {
     free(s->expanded);
     free(s->nbr);
     free(s->tmp);
+}
+
+static void free_search_scratch(orc_hnsw* h) {
+    scratch_t* scr = (scratch_t*)h->sscr;
+    for (int t = 0; scr && t < h->sscr_n; ++t) scratch_free(&scr[t]);
+    free(scr);
+    h->sscr = NULL;
+    h->sscr_n = 0;
 }
 
 static inline void scratch_newgen(scratch_t* s) {
@@ -814,16 +828,25 @@ int orc_hnsw_search(const orc_hnsw* h, const float* queries, size_t nq, size_t k
     if (ef < k) ef = k; /* usearch: expansion = max(expansion_search, wanted) */
     threads = resolve_threads(threads);
     if ((size_t)threads > nq) threads = nq ? (int)nq : 1;
-    scratch_t* scr = (scratch_t*)malloc(sizeof(scratch_t) * threads);
-    for (int t = 0; t < threads; ++t) scratch_init(&scr[t], h->slots, ef, h->M0);
+    /* per-thread scratch is cached on the index so repeated searches (the CPU
+     * baseline's timed calls) do not pay the visited-array allocation */
+    orc_hnsw* hm = (orc_hnsw*)h;
+    scratch_t* scr = (scratch_t*)hm->sscr;
+    if (!scr || hm->sscr_n < threads || hm->sscr_slots < h->slots || hm->sscr_ef < ef) {
+        for (int t = 0; scr && t < hm->sscr_n; ++t) scratch_free(&scr[t]);
+        free(scr);
+        scr = (scratch_t*)malloc(sizeof(scratch_t) * threads);
+        for (int t = 0; t < threads; ++t) scratch_init(&scr[t], h->slots, ef, h->M0);
+        hm->sscr = scr;
+        hm->sscr_n = threads;
+        hm->sscr_slots = h->slots;
+        hm->sscr_ef = ef;
+    }
+    for (int t = 0; t < threads; ++t) scr[t].ndist = 0;
     search_ctx c = {h, queries, k, ef, out_keys, out_dist, out_counts, scr};
     parallel_for(nq, threads, search_one, &c);
     uint64_t nd = 0;
-    for (int t = 0; t < threads; ++t) {
-        nd += scr[t].ndist;
-        scratch_free(&scr[t]);
-    }
-    free(scr);
+    for (int t = 0; t < threads; ++t) nd += scr[t].ndist;
     if (out_ndist) *out_ndist = nd;
     return 0;
 }

@@ -230,10 +230,12 @@ def test_edge_cases():
 
 
 def test_large_scale_properties():
-    """200k x 128 integer data: build, then size-independent properties."""
+    """200k x 128 SIFT-like integer data (f16 storage, C4 shape): build, then
+    size-independent properties."""
     n, dim = 200_000, 128
-    x = G.uint8_valued(n, dim, 51)
-    q = G.uint8_valued(500, dim, 52)
+    bs, qs, ms = G.config_seeds(3)
+    x = G.sift_like(n, dim, bs, ms)
+    q = G.sift_like(500, dim, qs, ms)
     idx = vsg.Index(dim, "l2sq", "f16", 16, 128, 64, seed=1)
     idx.add(np.arange(n), x)
     ex = idx.exact_search(q, 10)
@@ -280,6 +282,9 @@ def test_datagen_device_matches_numpy():
     np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4)
     u = vsg.datagen_device("uint8", 100, 16, 5).cpu().numpy()
     np.testing.assert_array_equal(u, G.uint8_valued(100, 16, 5))
+    s = vsg.datagen_device("sift", 200, 128, bs, ms).cpu().numpy()
+    ref = G.sift_like(200, 128, bs, ms)
+    assert np.mean(s == ref) > 0.999 and np.abs(s - ref).max() <= 1
     torch.cuda.synchronize()
 
 

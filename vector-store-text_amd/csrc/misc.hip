@@ -144,11 +144,16 @@ __global__ void gen_u8_kernel(size_t n, int dim, uint64_t seed, size_t start, fl
     out[i] = (float)(splitmix64(b + start * (uint64_t)dim + i) % 256);
 }
 
+__global__ void sift_transform_kernel(size_t tot, float* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < tot) out[i] = fminf(255.f, rintf(fmaxf(out[i], 0.f) * 48.f));
+}
+
 hipError_t launch_datagen(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed, size_t start_row,
                           float* out, float* scratch_w, float* scratch_c, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const size_t tot = n * dim;
-    if (kind == 0) {
+    if (kind == 0 || kind == 3) {
         const size_t nw = (size_t)LATENT * dim, ncen = (size_t)N_CENTRES * LATENT;
         hipLaunchKernelGGL(gen_normal_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s,
                            splitmix64(model_seed ^ TAG_PROJ), nw, 8.0f, scratch_w);
@@ -156,6 +161,8 @@ hipError_t launch_datagen(int kind, size_t n, size_t dim, uint64_t seed, uint64_
                            splitmix64(model_seed ^ TAG_CENTRE), ncen, 1.0f, scratch_c);
         hipLaunchKernelGGL(gen_clustered_kernel, dim3((unsigned)n), dim3(64), 0, s, n, (int)dim, seed, start_row,
                            scratch_w, scratch_c, out);
+        if (kind == 3)
+            hipLaunchKernelGGL(sift_transform_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, tot, out);
     } else if (kind == 1) {
         hipLaunchKernelGGL(gen_gauss_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, n, (int)dim,
                            seed, start_row, out);

@@ -795,10 +795,10 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
 
 int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed, size_t start_row,
                        float* out, void* stream) {
-    if (kind < 0 || kind > 2 || dim == 0) return fail(VSG_EINVAL, "bad datagen arguments");
+    if (kind < 0 || kind > 3 || dim == 0) return fail(VSG_EINVAL, "bad datagen arguments");
     hipStream_t s = (hipStream_t)stream;
     float *w = nullptr, *c = nullptr;
-    if (kind == 0) {
+    if (kind == 0 || kind == 3) {
         HIP_TRY(hipMallocAsync((void**)&w, 64 * dim * 4, s));
         HIP_TRY(hipMallocAsync((void**)&c, 1024 * 64 * 4, s));
     }

@@ -79,6 +79,13 @@ def lib() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"libvsg.so not built at {LIB_PATH}: run `make -C vector-store-text_amd` "
                            "(or __graft_entry__.build()); there is no CPU fallback")
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same
+    # soname as /opt/rocm's).  Loading torch first makes libvsg bind to that copy,
+    # so device pointers and hipStream_t handles are shared with torch.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     P, sz, u64, u32 = C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint32
     sigs = {

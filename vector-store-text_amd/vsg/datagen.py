@@ -95,5 +95,15 @@ def uint8_valued(n: int, dim: int, seed: int, start: int = 0) -> np.ndarray:
     return (r % np.uint64(256)).astype(np.float32)
 
 
+SIFT_SCALE = 48.0
+
+
+def sift_like(n: int, dim: int, seed: int, model_seed: int, start: int = 0) -> np.ndarray:
+    """Clustered-latent rows, ReLU, scaled by 48 and rounded into 0..255 (SIFT
+    shape): integer-valued, so exact in f16 and in f32 sums."""
+    y = clustered(n, dim, seed, model_seed, start)
+    return np.clip(np.rint(np.maximum(y, 0.0) * SIFT_SCALE), 0, 255).astype(np.float32)
+
+
 def config_seeds(config: int):
     return 0x5EED0000 + config, 0x5EED1000 + config, 0x5EED2000 + config

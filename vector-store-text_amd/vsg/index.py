@@ -200,7 +200,7 @@ def merge_topk_device(keys_t, dist_t, k, stream=None):
 def datagen_device(kind: str, n: int, dim: int, seed: int, model_seed: int = 0, start: int = 0,
                    out=None, stream=None):
     import torch
-    kinds = {"clustered": 0, "gaussian": 1, "uint8": 2}
+    kinds = {"clustered": 0, "gaussian": 1, "uint8": 2, "sift": 3}
     if out is None:
         out = torch.empty((n, dim), dtype=torch.float32, device="cuda")
     check(lib().vsg_datagen_device(kinds[kind], n, dim, seed, model_seed, start, _tp(out),

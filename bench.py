@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--metric", default="cos")
     ap.add_argument("--queries", type=int, default=10_000)
@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--config", type=int, default=1, help="seed set (BASELINE.json configs index)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo: rehearse several ranks on one GPU (collectives via host)")
     return ap.parse_args()
 
 
@@ -62,13 +64,19 @@ def main():
     import vsg
     from vsg import datagen as G
 
+    from vsg.distributed import gather_topk, merge_topk
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())  # >1 rank per GPU only for gloo rehearsal
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.dist_backend)
 
     def barrier():
         if world > 1:
@@ -78,12 +86,12 @@ def main():
     def max_over_ranks(x: float) -> float:
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     bs, qs, ms = G.config_seeds(a.config)
-    lo, hi = rank * a.n // world, (rank + 1) * a.n // world
+    lo, hi = rank * a.rows // world, (rank + 1) * a.rows // world
     nloc = hi - lo
     stream = torch.cuda.current_stream()
 
@@ -100,18 +108,15 @@ def main():
     index.add_device(np.arange(lo, hi, dtype=np.uint64), x, stream=stream)
     torch.cuda.synchronize()
     build_s = max_over_ranks(time.perf_counter() - t0)
-    build_vps = a.n / build_s
+    build_vps = a.rows / build_s
     bstats = index.stats()
 
     def sharded(qt, ef, exact=False):
         keys, dists = index.search_device(qt, a.k, ef, stream=stream, exact=exact)
         if world == 1:
             return keys, dists
-        gk = torch.empty((world,) + tuple(keys.shape), dtype=keys.dtype, device=dev)
-        gd = torch.empty((world,) + tuple(dists.shape), dtype=dists.dtype, device=dev)
-        dist.all_gather_into_tensor(gk, keys)
-        dist.all_gather_into_tensor(gd, dists)
-        return vsg.merge_topk_device(gk, gd, a.k, stream=stream)
+        gk, gd = gather_topk(keys, dists)
+        return merge_topk(gk, gd, a.k, stream=stream)
 
     # ---- ground truth (exact, GPU brute force, same sharded merge path)
     qgt = q[: a.gt_queries].contiguous()
@@ -128,16 +133,29 @@ def main():
         ef = a.ef
         sweep.append((ef, recall_of(sharded(qgt, ef)[0])))
     else:
-        ef = None
+        ef, lo_fail = None, None
         for cand in (16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512):
             r = recall_of(sharded(qgt, cand)[0])
             sweep.append((cand, r))
             if r >= a.target_recall:
                 ef = cand
                 break
+            lo_fail = cand
         if ef is None:
             ef = sweep[-1][0]
-    recall = sweep[-1][1]
+        elif lo_fail is not None:
+            # smallest ef in (lo_fail, ef] that still meets the target
+            e_lo, e_hi = lo_fail, ef
+            while e_hi - e_lo > 2:
+                mid = (e_lo + e_hi) // 2
+                r = recall_of(sharded(qgt, mid)[0])
+                sweep.append((mid, r))
+                if r >= a.target_recall:
+                    e_hi = mid
+                else:
+                    e_lo = mid
+            ef = e_hi
+    recall = dict(sweep)[ef]
 
     # ---- timed QPS steps
     for _ in range(a.warmup):
@@ -153,11 +171,8 @@ def main():
         keys, dists = index.search_device(q, a.k, ef, stream=stream)
         ev1.record(stream)
         if world > 1:
-            gk = torch.empty((world,) + tuple(keys.shape), dtype=keys.dtype, device=dev)
-            gd = torch.empty((world,) + tuple(dists.shape), dtype=dists.dtype, device=dev)
-            dist.all_gather_into_tensor(gk, keys)
-            dist.all_gather_into_tensor(gd, dists)
-            keys, dists = vsg.merge_topk_device(gk, gd, a.k, stream=stream)
+            gk, gd = gather_topk(keys, dists)
+            keys, dists = merge_topk(gk, gd, a.k, stream=stream)
         torch.cuda.synchronize()
         kern_ms += ev0.elapsed_time(ev1)
     barrier()
@@ -183,14 +198,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py), 10k queries/step",
-        "config": {"workload": f"C2: {a.n} x {a.dim} f32 {a.metric} HNSW M={a.M} efC={a.efc} k={a.k}",
-                   "index_rows": a.n, "dim": a.dim, "queries_per_step": a.queries,
+        "config": {"workload": f"C2: {a.rows} x {a.dim} f32 {a.metric} HNSW M={a.M} efC={a.efc} k={a.k}",
+                   "index_rows": a.rows, "dim": a.dim, "queries_per_step": a.queries,
                    "ef": ef, "recall_at_10": round(recall, 4), "ef_sweep": sweep,
                    "parallelism": f"row-shard x{world}" + (" + RCCL all-gather top-k" if world > 1 else "")},
         "build_vectors_per_s": round(build_vps, 1),
         "build_seconds": round(build_s, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic(a, ef),
                      "kernel": "hnsw_search_kernel<64,3,4,float,1>", "kernel_ms": round(kern_ms_avg, 3),
                      "alg_bytes_per_launch": int(alg_bytes),
                      "dist_evals_per_query": round(st["search_distances"] / max(1, st["search_queries"]), 1)},
@@ -207,6 +223,33 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(a, ef):
+    """HBM bytes per search launch from the committed rocprofv3 PMC summary
+    (profiles/search_pmc.json, written by tools/pmc_summary.py from separate
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this same workload, gfx950 x2
+    FETCH_SIZE correction applied there), or None when it does not match."""
+    p = os.path.join(ROOT, "profiles", "search_pmc.json")
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    w = d.get("workload", {})
+    if (w.get("n"), w.get("dim"), w.get("queries"), w.get("ef"), w.get("metric")) != (
+            a.rows, a.dim, a.queries, ef, a.metric):
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def host_cores() -> int:
@@ -235,7 +278,7 @@ def cpu_baseline(a, index, q_t, ef, x_t):
 
     O.set_fast_metric(True)
     threads = host_cores()
-    res = {"unit": "queries/s", "cores": threads, "kind": "port"}
+    res = {"unit": "queries/s", "cores": threads, "kind": "port", "cpu": cpu_model()}
     # (1) search QPS: the same graph, exported from HBM, searched by the C restatement
     g = index.export()
     h = O.HnswOracle(a.dim, a.metric, a.M, a.efc, ef)

@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--config", type=int, default=1, help="seed set (BASELINE.json configs index)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--quant", default="f32", choices=("f32", "f16"), help="HBM storage type")
+    ap.add_argument("--sort-queries", default="none", choices=("none", "cluster"),
+                    help="experiment: order the query batch by synthetic cluster id")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse several ranks on one GPU (collectives via host)")
     return ap.parse_args()
@@ -98,10 +101,14 @@ def main():
     # ---- inputs in HBM
     x = vsg.datagen_device("clustered", nloc, a.dim, bs, ms, start=lo)
     q = vsg.datagen_device("clustered", a.queries, a.dim, qs, ms)
+    if a.sort_queries == "cluster":
+        cl = (G.splitmix64(G._stream(qs, G.TAG_CLUSTER) + np.arange(a.queries, dtype=np.uint64))
+              % np.uint64(G.N_CENTRES)).astype(np.int64)
+        q = q[torch.from_numpy(np.argsort(cl, kind="stable")).to(dev)].contiguous()
     torch.cuda.synchronize()
 
     # ---- build (timed; not part of the QPS step)
-    index = vsg.Index(a.dim, a.metric, "f32", a.M, a.efc, 128, device=local, seed=0x5EED + rank)
+    index = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 128, device=local, seed=0x5EED + rank)
     index.reserve(nloc)
     barrier()
     t0 = time.perf_counter()
@@ -180,7 +187,8 @@ def main():
     ms_per_step = 1000.0 * elapsed / a.steps
     qps = a.queries * a.steps / elapsed
     st = index.stats()
-    row_bytes = ((a.dim + 3) // 4) * 16
+    per16 = 4 if a.quant == "f32" else 8
+    row_bytes = ((a.dim + per16 - 1) // per16) * 16
     alg_bytes = (st["search_distances"] * row_bytes + st["search_adjacency"] * 2 * a.M * 4) / a.steps
     kern_ms_avg = kern_ms / a.steps
     achieved = alg_bytes / (kern_ms_avg * 1e-3) / 1e9
@@ -196,7 +204,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": a.quant,
         "data": "synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py), 10k queries/step",
         "config": {"workload": f"C2: {a.rows} x {a.dim} f32 {a.metric} HNSW M={a.M} efC={a.efc} k={a.k}",
                    "index_rows": a.rows, "dim": a.dim, "queries_per_step": a.queries,

@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--config", type=int, default=1, help="seed set (BASELINE.json configs index)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mode", default="hnsw", choices=("hnsw", "exact"),
+                    help="exact: brute-force MFMA path (C5: --rows 1000000 --dim 1536 --metric ip)")
+    ap.add_argument("--batch", type=int, default=1024, help="exact mode: queries per step")
     ap.add_argument("--quant", default="f32", choices=("f32", "f16"), help="HBM storage type")
     ap.add_argument("--sort-queries", default="none", choices=("none", "cluster"),
                     help="experiment: order the query batch by synthetic cluster id")
@@ -106,6 +109,9 @@ def main():
               % np.uint64(G.N_CENTRES)).astype(np.int64)
         q = q[torch.from_numpy(np.argsort(cl, kind="stable")).to(dev)].contiguous()
     torch.cuda.synchronize()
+
+    if a.mode == "exact":
+        return run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_over_ranks)
 
     # ---- build (timed; not part of the QPS step)
     index = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 128, device=local, seed=0x5EED + rank)
@@ -231,6 +237,89 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+
+
+def run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_over_ranks):
+    """Brute-force mode: one step = exact top-k of a batch of
+    queries over the whole index on the f32 matrix cores; roofline bound = MFMA."""
+    import torch
+
+    import vsg
+    from vsg.distributed import gather_topk, merge_topk
+
+    nloc = hi - lo
+    index = vsg.Index(a.dim, a.metric, a.quant, device=local, exact_only=True)
+    index.add_device(np.arange(lo, hi, dtype=np.uint64), x, stream=stream)
+    qb = q[: a.batch].contiguous()
+
+    def step():
+        keys, dists = index.search_device(qb, a.k, stream=stream, exact=True)
+        if world > 1:
+            gk, gd = gather_topk(keys, dists)
+            keys, dists = merge_topk(gk, gd, a.k, stream=stream)
+        return keys, dists
+
+    for _ in range(a.warmup):
+        step()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kern_ms = 0.0
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ev0.record(stream)
+        keys, dists = index.search_device(qb, a.k, stream=stream, exact=True)
+        ev1.record(stream)
+        if world > 1:
+            gk, gd = gather_topk(keys, dists)
+            keys, dists = merge_topk(gk, gd, a.k, stream=stream)
+        torch.cuda.synchronize()
+        kern_ms += ev0.elapsed_time(ev1)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    qps = a.batch * a.steps / elapsed
+    kms = kern_ms / a.steps
+    flops = 2.0 * a.batch * nloc * a.dim
+    tflops = flops / (kms * 1e-3) / 1e12
+    out = {
+        "metric": f"brute-force kNN QPS (exact, f32 MFMA), {a.rows} x {a.dim} f32 {a.metric}, batch {a.batch}",
+        "value": round(qps, 1), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(1000 * elapsed / a.steps, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py)",
+        "config": {"workload": f"C5: {a.rows} x {a.dim} f32 {a.metric} brute force, k={a.k}",
+                   "batch": a.batch, "parallelism": f"row-shard x{world}"},
+        "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": MFMA_F32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(tflops / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel": "mfma_exact_kernel<16,MET> (+prepare, merge)", "kernel_ms": round(kms, 3),
+                     "flops_per_launch": flops},
+    }
+    if world == 1 and rank == 0 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+
+        O.set_fast_metric(True)
+        threads = host_cores()
+        xh = x.cpu().numpy()
+        qh = qb.cpu().numpy()
+        n = 4
+        t0 = time.perf_counter()
+        ok, od, _ = O.exact_search(a.metric, xh, qh[:n], a.k, threads=threads)
+        dt = time.perf_counter() - t0
+        n2 = int(min(a.batch, max(n, n * a.cpu_seconds / max(dt, 1e-6))))
+        t0 = time.perf_counter()
+        ok, od, _ = O.exact_search(a.metric, xh, qh[:n2], a.k, threads=threads)
+        dt = time.perf_counter() - t0
+        gk = keys[:n2].cpu().numpy().view(np.uint64)
+        agree = float(np.mean([len(set(gk[i]) & set(ok[i])) / a.k for i in range(n2)]))
+        out["cpu_baseline"] = {"value": round(n2 / dt, 2), "unit": "queries/s", "cores": threads, "kind": "port",
+                               "cpu": cpu_model(),
+                               "sample": f"{n2} queries, exact scan of {a.rows} rows, SIMD f32, {threads} threads"}
+        out["parity_sample_recall_vs_oracle"] = round(agree, 5)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def pmc_traffic(a, ef):

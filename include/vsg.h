@@ -47,6 +47,10 @@ extern "C" {
 
 #define VSG_NO_KEY UINT64_MAX /* padding key for short result rows */
 
+/* flags: store vectors only (no HNSW graph); exact_search works, search returns
+ * VSG_EUNSUPPORTED.  The brute-force MFMA configuration. */
+#define VSG_FLAG_EXACT_ONLY 1u
+
 typedef struct vsg_index vsg_index_t;
 
 /* Mirrors usearch::IndexOptions as built at src/index/usearch.rs:89-96.
@@ -61,7 +65,7 @@ typedef struct {
     uint32_t expansion_add;    /* ExpansionAdd (efC), src/lib.rs:181-182; 0 => 128 */
     uint32_t expansion_search; /* ExpansionSearch (ef), src/lib.rs:199-200; 0 => 64 */
     int32_t device;            /* HIP device ordinal (one shard per GPU) */
-    uint32_t flags;            /* reserved, 0 */
+    uint32_t flags;            /* VSG_FLAG_*, 0 = HNSW index */
     uint64_t seed;             /* level-sampling seed */
 } vsg_index_options_t;
 

@@ -73,6 +73,50 @@ def test_exact_matches_oracle_with_tombstones_and_keys():
     np.testing.assert_array_equal(m.distances, od)
 
 
+@pytest.mark.parametrize("metric,dim,n,nq,k", [("l2sq", 64, 3001, 33, 10), ("ip", 96, 5000, 200, 16),
+                                               ("l2sq", 128, 1000, 257, 1), ("ip", 32, 130, 40, 7)])
+def test_exact_mfma_bitexact_integer(metric, dim, n, nq, k, monkeypatch):
+    """f32-MFMA brute force (nq >= 32, k <= 16, dim % 32 == 0) vs the oracle, with
+    tombstones, ragged tiles (n, nq not multiples of 128) and non-trivial keys."""
+    scale = 16.0 if metric == "ip" else 1.0
+    x = G.uint8_valued(n, dim, 81) / scale
+    q = G.uint8_valued(nq, dim, 82) / scale
+    keys = np.arange(n, dtype=np.uint64) * 3 + 11
+    idx = vsg.Index(dim, metric)
+    idx.add(keys, x)
+    idx.remove(keys[::7])
+    removed = np.zeros(n, np.uint8)
+    removed[::7] = 1
+    ok, od, oc = O.exact_search(metric, x, q, k, keys=keys, removed=removed)
+    monkeypatch.setenv("VSG_EXACT_MFMA", "1")
+    m = idx.exact_search(q, k)
+    monkeypatch.setenv("VSG_EXACT_MFMA", "0")
+    v = idx.exact_search(q, k)
+    for res in (m, v):
+        np.testing.assert_array_equal(res.keys, ok)
+        np.testing.assert_array_equal(res.distances, od)
+        np.testing.assert_array_equal(res.counts, oc)
+
+
+@pytest.mark.parametrize("metric,dim", [("cos", 768), ("l2sq", 1536), ("ip", 256)])
+def test_exact_mfma_float_vs_valu(metric, dim, monkeypatch):
+    bs, qs, ms = G.config_seeds(4)
+    x = G.clustered(4000, dim, bs, ms)
+    q = G.clustered(150, dim, qs, ms)
+    idx = vsg.Index(dim, metric)
+    idx.add(np.arange(4000), x)
+    monkeypatch.setenv("VSG_EXACT_MFMA", "1")
+    m = idx.exact_search(q, 10)
+    monkeypatch.setenv("VSG_EXACT_MFMA", "0")
+    v = idx.exact_search(q, 10)
+    scale = np.maximum(1.0, np.abs(v.distances))
+    assert np.max(np.abs(m.distances - v.distances) / scale) < 2e-4
+    gk, gd, _ = O.exact_search(metric, x, q, 11)
+    for i in range(q.shape[0]):
+        if not np.array_equal(m.keys[i], v.keys[i]):
+            assert gd[i][10] - gd[i][9] < 1e-3 or np.min(np.diff(gd[i])) < 1e-3
+
+
 # -------------------------------------------------------------- reference KATs --
 
 def _kats():

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(64) void merge_parts_kernel(MergeParams p) {
     L.size = 0;
     float* sd = reinterpret_cast<float*>(s);
     uint32_t* si = reinterpret_cast<uint32_t*>(s + 256);
-    const size_t total = (size_t)p.parts * p.k;
+    const size_t total = (size_t)p.parts * (p.kin ? p.kin : p.k);
     const float* pd = p.part_d + (size_t)qi * total;
     const uint32_t* pi = p.part_i + (size_t)qi * total;
     for (size_t t = 0; t < total; t += 64) {

@@ -1,0 +1,213 @@
+// mfma_exact.hip — batched brute-force k-NN on the f32 matrix cores (gfx950).
+//
+// The only dense contraction on this path:
+// D = X . Q^T with `v_mfma_f32_32x32x2_f32` (exact f32 FMA chain, 64 FLOP/clk/SIMD),
+// fused with a per-lane register top-KMAX so no distance tile ever reaches HBM.
+//
+//   block = 256 threads (4 waves, 2 x 2), tile = 128 base rows x 128 queries,
+//   K stage = 32 dims, double-buffered LDS [rows | queries][32 + 4 pad] floats
+//   (row stride 36 dwords: the 16-lane groups of ds_read_b128 hit disjoint banks),
+//   register-staged global loads issued before the MFMAs of the current stage
+//   and written to the other LDS buffer after them (one barrier per stage).
+//   Wave (wr, wq) owns rows [wr*64, +64) x queries [wq*64, +64) = 2 x 2 MFMA tiles.
+//   A operand = base rows, B operand = queries, so C lane l holds query (l & 31)
+//   against 16 rows: each lane keeps a sorted top-KMAX per query in VGPRs.
+//   Within a K stage the half-wave h takes dims [h*16, h*16+16): a lane reads 16
+//   contiguous floats per fragment (4 x ds_read_b128) instead of a stride-2 gather.
+//
+// Grid: (query tile, row split) pairs, mapped XCD-contiguously (blocks b, b+8, ...
+// share an XCD) so the query tiles of one row split run on one XCD and share the
+// base rows through its L2.  Partial lists [q][part][KMAX], part = (split, wr, h),
+// are merged by merge_parts_kernel.  Ties: (distance, slot) as everywhere.
+#include <hip/hip_runtime.h>
+
+#include "vsg_device.hpp"
+#include "vsg_kernels.hpp"
+
+namespace vsg {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int KT = 32;   // dims per stage = one 128-B LDS row
+constexpr int LDK = 32;  // LDS row stride (floats), unpadded: glds writes lane-linear 1-KiB pieces
+constexpr int STAGE_FLOATS = (MFMA_BR + MFMA_BQ) * LDK;
+constexpr size_t MFMA_LDS_BYTES = 2 * STAGE_FLOATS * sizeof(float);
+
+// 16-B slot of logical chunk c (0..7) in LDS row R: XOR swizzle so the sixteen
+// lanes of a ds_read_b128 group (rows R..R+15, same chunk) hit distinct slots of
+// the 64-bank row (conflict-free); applied to the glds SOURCE and to the read.
+__device__ __forceinline__ int swz(int R, int c) { return c ^ ((R >> 1) & 7); }
+
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+template <int KMAX>
+__device__ __forceinline__ void topk_insert(float (&ld)[KMAX], uint32_t (&li)[KMAX], float d, uint32_t id) {
+    // ascending list, strict < : an equal distance from a later (larger) slot goes after
+#pragma unroll
+    for (int t = KMAX - 1; t >= 1; --t) {
+        const bool shift = d < ld[t - 1];
+        const bool here = !shift && d < ld[t];
+        ld[t] = shift ? ld[t - 1] : (here ? d : ld[t]);
+        li[t] = shift ? li[t - 1] : (here ? id : li[t]);
+    }
+    if (d < ld[0]) {
+        ld[0] = d;
+        li[0] = id;
+    }
+}
+
+template <int KMAX, int MET>
+__global__ __launch_bounds__(256, 2) void mfma_exact_kernel(MfmaExactParams p) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = tid >> 6;
+    const int wq = w & 1, wr = w >> 1;
+    const int h = lane >> 5, r = lane & 31;
+
+    // XCD-contiguous block -> (split, query tile)
+    const int nb = gridDim.x;
+    const int per = nb >> 3;
+    const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (L >= p.qtiles * p.splits) return;
+    const int split = L / p.qtiles;
+    const int qt = L % p.qtiles;
+    const int q0 = qt * MFMA_BQ;
+    const size_t ntiles = (p.nslots + MFMA_BR - 1) / MFMA_BR;
+    const size_t t_beg = (size_t)split * p.tiles_per_split;
+    const size_t t_end = min(t_beg + (size_t)p.tiles_per_split, ntiles);
+    const int nst = (p.row_floats + KT - 1) / KT;
+
+    float ld[2][KMAX];
+    uint32_t li[2][KMAX];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int t = 0; t < KMAX; ++t) {
+            ld[b][t] = __builtin_inff();
+            li[b][t] = VSG_EMPTY;
+        }
+
+    float qs2[2] = {0.f, 0.f};
+    if constexpr (MET == MET_L2) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int qi = q0 + wq * 64 + b * 32 + r;
+            qs2[b] = qi < p.nq ? p.qsqnorm[qi] : 0.f;
+        }
+    }
+
+    for (size_t tile = t_beg; tile < t_end; ++tile) {
+        const size_t r0 = tile * MFMA_BR;
+        floatx16 acc[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) acc[a][b][g] = 0.f;
+
+        // LDS-DMA staging: wave w fills 1-KiB pieces w*4+u (8 rows x 128 B) of the
+        // base-row and query tiles; out-of-range rows read a clamped valid row
+        // (masked in the epilogue / never written out).
+        const int prow = lane >> 3, pslot = lane & 7;
+        auto load_stage = [&](int s, int buf) {
+            const int k0 = s * KT;
+            float* xs = lds + buf * STAGE_FLOATS;
+            float* qs = xs + MFMA_BR * LDK;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int piece = w * 4 + u;
+                const int R = piece * 8 + prow;
+                const int c = swz(R, pslot);
+                const size_t grow = min(r0 + (size_t)R, p.nslots - 1);
+                const size_t gq = (size_t)min(q0 + R, p.nq - 1);
+                __builtin_amdgcn_global_load_lds((gptr_t)(p.vecs + grow * p.row_floats + k0 + c * 4),
+                                                 (lptr_t)(xs + piece * 8 * LDK), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((gptr_t)(p.queries + gq * p.row_floats + k0 + c * 4),
+                                                 (lptr_t)(qs + piece * 8 * LDK), 16, 0, 0);
+            }
+        };
+
+        load_stage(0, 0);
+        __syncthreads();  // drains the LDS-DMA (vmcnt(0)) and publishes stage 0
+        for (int s = 0; s < nst; ++s) {
+            const int buf = s & 1;
+            if (s + 1 < nst) load_stage(s + 1, buf ^ 1);  // buf^1 was last read before the previous barrier
+            const float* xs = lds + buf * STAGE_FLOATS;
+            const float* qs = xs + MFMA_BR * LDK;
+#pragma unroll
+            for (int tq = 0; tq < 4; ++tq) {
+                float4 xa[2], qb[2];
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    const int R = wr * 64 + a * 32 + r;
+                    xa[a] = *reinterpret_cast<const float4*>(xs + R * LDK + swz(R, h * 4 + tq) * 4);
+                }
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const int R = wq * 64 + b * 32 + r;
+                    qb[b] = *reinterpret_cast<const float4*>(qs + R * LDK + swz(R, h * 4 + tq) * 4);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int b = 0; b < 2; ++b) {
+                            const float av = e == 0 ? xa[a].x : e == 1 ? xa[a].y : e == 2 ? xa[a].z : xa[a].w;
+                            const float bv = e == 0 ? qb[b].x : e == 1 ? qb[b].y : e == 2 ? qb[b].z : qb[b].w;
+                            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[a][b], 0, 0, 0);
+                        }
+                }
+            }
+            __syncthreads();
+        }
+
+        // epilogue: distances + register top-KMAX (rows arrive in increasing slot order)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const size_t row = r0 + wr * 64 + a * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+                const bool valid = row < p.nslots && !(p.flags[row < p.nslots ? row : 0] & 1);
+                float xs2 = 0.f;
+                if constexpr (MET == MET_L2) xs2 = valid ? p.sqnorm[row] : 0.f;
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const float dot = acc[a][b][g];
+                    float d = (MET == MET_L2) ? (xs2 + qs2[b]) - 2.f * dot : 1.f - dot;
+                    if (!valid) d = __builtin_inff();
+                    if (d < ld[b][KMAX - 1]) topk_insert<KMAX>(ld[b], li[b], d, (uint32_t)row);
+                }
+            }
+        }
+    }
+
+    const int nparts = p.splits * 4;
+    const int part = (split * 2 + wr) * 2 + h;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int qi = q0 + wq * 64 + b * 32 + r;
+        if (qi >= p.nq) continue;
+        const size_t o = ((size_t)qi * nparts + part) * KMAX;
+#pragma unroll
+        for (int t = 0; t < KMAX; ++t) {
+            p.part_d[o + t] = ld[b][t];
+            p.part_i[o + t] = ld[b][t] < __builtin_inff() ? li[b][t] : VSG_EMPTY;
+        }
+    }
+}
+
+hipError_t launch_mfma_exact(MetricKind mk, const MfmaExactParams& p, hipStream_t s) {
+    if (p.kmax != 16) return hipErrorNotSupported;
+    const int total = p.qtiles * p.splits;
+    const int nb = (total + 7) / 8 * 8;
+    auto kern = mk == MK_L2 ? mfma_exact_kernel<16, MET_L2> : mfma_exact_kernel<16, MET_DOT>;
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)MFMA_LDS_BYTES);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(256), MFMA_LDS_BYTES, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace vsg

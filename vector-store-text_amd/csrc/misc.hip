@@ -12,7 +12,7 @@ namespace vsg {
 template <typename T>
 __global__ __launch_bounds__(256) void prepare_kernel(const float* __restrict__ in, size_t n, int dim,
                                                       int normalize, uint8_t* __restrict__ out,
-                                                      size_t row_bytes) {
+                                                      size_t row_bytes, float* __restrict__ sqnorm) {
     const size_t row = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= n) return;
@@ -27,10 +27,18 @@ __global__ __launch_bounds__(256) void prepare_kernel(const float* __restrict__ 
         nrm = sqrtf(s);
     }
     const int padded = (int)(row_bytes / sizeof(T));
+    float s2 = 0.f;
     for (int j = lane; j < padded; j += 64) {
         float v = 0.f;
         if (j < dim) v = (normalize && nrm > 0.f) ? x[j] / nrm : (normalize ? 0.f : x[j]);
-        y[j] = (T)v;
+        const T t = (T)v;
+        y[j] = t;
+        s2 += (float)t * (float)t;
+    }
+    if (sqnorm) {  // |stored row|^2 for the MFMA L2 expansion |x|^2 + |q|^2 - 2 x.q
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+        if (lane == 0) sqnorm[row] = s2;
     }
 }
 
@@ -45,14 +53,15 @@ __global__ void unprepare_kernel(const uint8_t* __restrict__ in, size_t n, int d
 }
 
 hipError_t launch_prepare(Storage st, const float* in, size_t n, int dim, bool normalize, uint8_t* out,
-                          size_t row_bytes, hipStream_t s) {
+                          size_t row_bytes, hipStream_t s, float* sqnorm) {
     if (n == 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 3) / 4));
     if (st == ST_F32)
-        hipLaunchKernelGGL(prepare_kernel<float>, grid, dim3(256), 0, s, in, n, dim, normalize ? 1 : 0, out, row_bytes);
+        hipLaunchKernelGGL(prepare_kernel<float>, grid, dim3(256), 0, s, in, n, dim, normalize ? 1 : 0, out, row_bytes,
+                           sqnorm);
     else
         hipLaunchKernelGGL(prepare_kernel<_Float16>, grid, dim3(256), 0, s, in, n, dim, normalize ? 1 : 0, out,
-                           row_bytes);
+                           row_bytes, sqnorm);
     return hipGetLastError();
 }
 

@@ -110,6 +110,7 @@ struct vsg_index {
     size_t upper_cap = 0, upper_used = 0;
     uint64_t* d_keys = nullptr;
     uint8_t* d_flags = nullptr;
+    float* d_sqnorm = nullptr;  // |stored row|^2 (MFMA exact L2 expansion)
     unsigned long long* d_stats = nullptr;  // [0..2] search, [3..4] build
 
     std::vector<int8_t> h_levels;
@@ -154,6 +155,7 @@ static void free_dev(vsg_index* h) {
     hipFree(h->d_upper);
     hipFree(h->d_keys);
     hipFree(h->d_flags);
+    hipFree(h->d_sqnorm);
     hipFree(h->d_stats);
     hipFree(h->d_blevels);
     hipFree(h->d_pair_off);
@@ -193,6 +195,7 @@ static int reserve_locked(vsg_index* h, size_t capacity) {
     if ((rc = grow_array(&h->d_upper_off, s, capacity, 0xFF, h->stream))) return rc;
     if ((rc = grow_array(&h->d_keys, s, capacity, 0xFF, h->stream))) return rc;
     if ((rc = grow_array(&h->d_flags, s, capacity, 0, h->stream))) return rc;
+    if ((rc = grow_array(&h->d_sqnorm, s, capacity, 0, h->stream))) return rc;
     h->h_levels.resize(capacity, 0);
     h->cap = capacity;
     return VSG_OK;
@@ -285,6 +288,10 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
     for (size_t i = 0; i < n; ++i) h->key2slot[keys[i]] = s0 + (uint32_t)i;
     h->slots += n;
     h->live += n;
+    if (h->opt.flags & VSG_FLAG_EXACT_ONLY) {  // vectors only: no graph
+        h->build_vectors += n;
+        return VSG_OK;
+    }
 
     if ((rc = ensure_nodes(h, n))) return rc;
     HIP_TRY(hipMemcpyAsync(h->d_blevels, h->h_levels.data() + s0, n, hipMemcpyHostToDevice, st));
@@ -486,7 +493,7 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
         HIP_TRY(hipStreamWaitEvent(h->stream, ev, 0));
         HIP_TRY(hipEventDestroy(ev));
         HIP_TRY(launch_prepare(h->st, vecs, n, h->dim, h->normalize, h->d_vecs + (size_t)s0 * h->row_bytes,
-                               h->row_bytes, h->stream));
+                               h->row_bytes, h->stream, h->d_sqnorm + s0));
     } else {
         const size_t chunk = 65536;
         if ((rc = ensure_buf(&h->d_stage, h->stage_cap, std::min(n, chunk) * h->dim))) return rc;
@@ -494,7 +501,8 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
             const size_t c = std::min(chunk, n - off);
             HIP_TRY(hipMemcpyAsync(h->d_stage, vecs + off * h->dim, c * h->dim * 4, hipMemcpyHostToDevice, h->stream));
             HIP_TRY(launch_prepare(h->st, h->d_stage, c, h->dim, h->normalize,
-                                   h->d_vecs + (size_t)(s0 + off) * h->row_bytes, h->row_bytes, h->stream));
+                                   h->d_vecs + (size_t)(s0 + off) * h->row_bytes, h->row_bytes, h->stream,
+                                   h->d_sqnorm + s0 + off));
             HIP_TRY(hipStreamSynchronize(h->stream));
         }
     }
@@ -542,10 +550,61 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
     if (k == 0) return fail(VSG_EINVAL, "k must be >= 1 (Limit is NonZeroUsize)");
     if (nq == 0) return VSG_OK;
     if (k > 1024) return fail(VSG_EUNSUPPORTED, "k > 1024");
+    if (!exact && (h->opt.flags & VSG_FLAG_EXACT_ONLY))
+        return fail(VSG_EUNSUPPORTED, "index was created with VSG_FLAG_EXACT_ONLY (no graph)");
+    // exact search on the f32 matrix cores when the batch amortises a 128-query tile
+    const size_t mfma_min = (size_t)env_double("VSG_EXACT_MFMA_MIN", 32);
+    const bool use_mfma = exact && h->st == ST_F32 && k <= 16 && (h->row_bytes / 4) % 32 == 0 &&
+                          nq >= mfma_min && h->slots > 0 && env_double("VSG_EXACT_MFMA", 1) != 0;
     uint8_t* qp = nullptr;
+    float* qsq = nullptr;
     HIP_TRY(hipMallocAsync((void**)&qp, nq * h->row_bytes, s));
-    HIP_TRY(launch_prepare(h->st, q_dev, nq, h->dim, h->normalize, qp, h->row_bytes, s));
-    if (!exact) {
+    if (use_mfma) HIP_TRY(hipMallocAsync((void**)&qsq, nq * 4, s));
+    HIP_TRY(launch_prepare(h->st, q_dev, nq, h->dim, h->normalize, qp, h->row_bytes, s, qsq));
+    if (use_mfma) {
+        const int qtiles = (int)((nq + MFMA_BQ - 1) / MFMA_BQ);
+        const size_t ntiles = (h->slots + MFMA_BR - 1) / MFMA_BR;
+        size_t splits = std::min<size_t>(ntiles, std::max<size_t>(1, (1024 + qtiles - 1) / qtiles));
+        const size_t tps = (ntiles + splits - 1) / splits;
+        splits = (ntiles + tps - 1) / tps;
+        const int kmax = 16, nparts = (int)splits * 4;
+        float* pd = nullptr;
+        uint32_t* pi = nullptr;
+        const size_t np = nq * (size_t)nparts * kmax;
+        HIP_TRY(hipMallocAsync((void**)&pd, np * 4, s));
+        HIP_TRY(hipMallocAsync((void**)&pi, np * 4, s));
+        MfmaExactParams mp{};
+        mp.vecs = reinterpret_cast<const float*>(h->d_vecs);
+        mp.sqnorm = h->d_sqnorm;
+        mp.queries = reinterpret_cast<const float*>(qp);
+        mp.qsqnorm = qsq;
+        mp.row_floats = (int)(h->row_bytes / 4);
+        mp.nq = (int)nq;
+        mp.nslots = h->slots;
+        mp.flags = h->d_flags;
+        mp.qtiles = qtiles;
+        mp.splits = (int)splits;
+        mp.tiles_per_split = (int)tps;
+        mp.kmax = kmax;
+        mp.part_d = pd;
+        mp.part_i = pi;
+        HIP_TRY(launch_mfma_exact(h->mk, mp, s));
+        MergeParams gp{};
+        gp.part_d = pd;
+        gp.part_i = pi;
+        gp.nq = (int)nq;
+        gp.parts = nparts;
+        gp.k = (int)k;
+        gp.kin = kmax;
+        gp.keys = h->d_keys;
+        gp.out_keys = ok;
+        gp.out_dist = od;
+        gp.out_counts = oc;
+        HIP_TRY(launch_merge_parts(gp, s));
+        HIP_TRY(hipFreeAsync(pd, s));
+        HIP_TRY(hipFreeAsync(pi, s));
+        HIP_TRY(hipFreeAsync(qsq, s));
+    } else if (!exact) {
         size_t e = ef ? ef : (size_t)h->ef;
         e = std::max(e, k);
         if (e > 1024) e = 1024;
@@ -771,7 +830,7 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
     float* d = nullptr;
     HIP_TRY(hipMalloc(&d, slots * h->dim * 4));
     HIP_TRY(hipMemcpyAsync(d, vectors, slots * h->dim * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_prepare(h->st, d, slots, h->dim, h->normalize, h->d_vecs, h->row_bytes, st));
+    HIP_TRY(launch_prepare(h->st, d, slots, h->dim, h->normalize, h->d_vecs, h->row_bytes, st, h->d_sqnorm));
     HIP_TRY(hipMemcpyAsync(h->d_keys, keys, slots * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_flags, removed, slots, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_adj0, adj0, slots * h->M0 * 4, hipMemcpyHostToDevice, st));

@@ -69,10 +69,29 @@ struct ExactParams {
     uint32_t* part_i;  // nq x nblocks x k
 };
 
+// Brute force on MFMA (f32 storage): Q (nq x D) . X^T (N x D) with a fused
+// per-lane register top-KMAX; partial lists [q][part][KMAX], part = (split, wr, half).
+struct MfmaExactParams {
+    const float* vecs;      // N x row_floats (prepared rows)
+    const float* sqnorm;    // N (L2 only)
+    const float* queries;   // nq x row_floats (prepared)
+    const float* qsqnorm;   // nq (L2 only)
+    int row_floats;
+    int nq;
+    size_t nslots;
+    const uint8_t* flags;
+    int qtiles, splits;
+    int tiles_per_split;    // 128-row tiles per split
+    int kmax;
+    float* part_d;
+    uint32_t* part_i;
+};
+
 struct MergeParams {
     const float* part_d;
     const uint32_t* part_i;
     int nq, parts, k;
+    int kin;  // entries per partial list (0 => k)
     const uint64_t* keys;  // slot -> key (NULL: ids are already keys, 64-bit inputs)
     uint64_t* out_keys;
     float* out_dist;
@@ -95,11 +114,14 @@ hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipSt
 hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s);
 hipError_t launch_exact(Storage st, MetricKind mk, const ExactParams& p, hipStream_t s);
 hipError_t launch_merge_parts(const MergeParams& p, hipStream_t s);
+// returns hipErrorNotSupported when the MFMA path does not apply (k > 32)
+hipError_t launch_mfma_exact(MetricKind mk, const MfmaExactParams& p, hipStream_t s);
+constexpr int MFMA_BQ = 128, MFMA_BR = 128;
 hipError_t launch_merge_topk64(const uint64_t* keys, const float* dist, int parts, int nq, int k,
                                uint64_t* out_keys, float* out_dist, hipStream_t s);
 // f32 rows (stride dim) -> storage rows (row_bytes), normalised when `normalize`
 hipError_t launch_prepare(Storage st, const float* in, size_t n, int dim, bool normalize,
-                          uint8_t* out, size_t row_bytes, hipStream_t s);
+                          uint8_t* out, size_t row_bytes, hipStream_t s, float* sqnorm_out = nullptr);
 // storage rows -> f32 rows (stride dim)
 hipError_t launch_unprepare(Storage st, const uint8_t* in, size_t n, int dim, size_t row_bytes,
                             float* out, hipStream_t s);

@@ -45,12 +45,12 @@ class Matches:
 class Index:
     def __init__(self, dimensions: int, metric: str = "l2sq", quantization: str = "f32",
                  connectivity: int = 0, expansion_add: int = 0, expansion_search: int = 0,
-                 device: int = 0, seed: int = 0):
+                 device: int = 0, seed: int = 0, exact_only: bool = False):
         self.dimensions = int(dimensions)
         self.metric = metric
         self.quantization = quantization
         opt = Options(self.dimensions, METRICS[metric], SCALARS[quantization], connectivity,
-                      expansion_add, expansion_search, device, 0, seed)
+                      expansion_add, expansion_search, device, 1 if exact_only else 0, seed)
         h = C.c_void_p()
         check(lib().vsg_index_new(C.byref(opt), C.byref(h)))
         self._h = h

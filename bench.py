@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--quant", default="f32", choices=("f32", "f16"), help="HBM storage type")
     ap.add_argument("--sort-queries", default="none", choices=("none", "cluster"),
                     help="experiment: order the query batch by synthetic cluster id")
+    ap.add_argument("--sort-base", default="none", choices=("none", "cluster"),
+                    help="experiment: insert base rows in synthetic-cluster order (spatial slot ids)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse several ranks on one GPU (collectives via host)")
     return ap.parse_args()
@@ -116,9 +118,15 @@ def main():
     # ---- build (timed; not part of the QPS step)
     index = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 128, device=local, seed=0x5EED + rank)
     index.reserve(nloc)
+    keys_np = np.arange(lo, hi, dtype=np.uint64)
+    if a.sort_base == "cluster":
+        cl = (G.splitmix64(G._stream(bs, G.TAG_CLUSTER) + keys_np) % np.uint64(G.N_CENTRES)).astype(np.int64)
+        order = np.argsort(cl, kind="stable")
+        x = x[torch.from_numpy(order).to(dev)].contiguous()
+        keys_np = keys_np[order]
     barrier()
     t0 = time.perf_counter()
-    index.add_device(np.arange(lo, hi, dtype=np.uint64), x, stream=stream)
+    index.add_device(keys_np, x, stream=stream)
     torch.cuda.synchronize()
     build_s = max_over_ranks(time.perf_counter() - t0)
     build_vps = a.rows / build_s

@@ -228,6 +228,31 @@ def test_hnsw_gpu_build_recall_vs_oracle(metric, dim, quant):
         assert rg >= rc - 0.005, (ef, rg, rc)
 
 
+@pytest.mark.parametrize("chunk", [None, 1000])
+def test_hnsw_build_cluster_sorted_insertion(chunk):
+    """Insertion order correlated with space (cluster-sorted CDC stream): the
+    batched build must not lose recall vs the sequential oracle on the same order."""
+    n, dim, nq = 20000, 64, 300
+    bs, qs, ms = G.config_seeds(2)
+    x = G.clustered(n, dim, bs, ms)
+    q = G.clustered(nq, dim, qs, ms)
+    cl = (G.splitmix64(G._stream(bs, G.TAG_CLUSTER) + np.arange(n, dtype=np.uint64))
+          % np.uint64(G.N_CENTRES)).astype(np.int64)
+    order = np.argsort(cl, kind="stable")
+    xs, keys = x[order], order.astype(np.uint64)
+    gk, _, _ = O.exact_search("l2sq", x, q, 10)
+    h = O.HnswOracle(dim, "l2sq", 16, 128, 64, seed=4)
+    h.add(keys, xs, threads=1)
+    idx = vsg.Index(dim, "l2sq", "f32", 16, 128, 64, seed=4)
+    step = chunk or n
+    for s in range(0, n, step):
+        idx.add(keys[s:s + step], xs[s:s + step])
+    for ef in (16, 64):
+        rc = recall(h.search(q, 10, ef)[0], gk, 10)
+        rg = recall(idx.search(q, 10, ef).keys, gk, 10)
+        assert rg >= rc - 0.01, (ef, rg, rc)
+
+
 def test_hnsw_incremental_adds_remove_and_readd():
     dim = 48
     x = G.uint8_valued(9000, dim, 41)

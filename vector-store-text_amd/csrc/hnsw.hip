@@ -227,7 +227,14 @@ __device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uin
 template <int G, int VM, int U, typename T, int MET>
 __global__ __launch_bounds__(64) void hnsw_search_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int qi = blockIdx.x;
+    int qi = blockIdx.x;
+    if (p.xcd_map) {
+        // bijective: XCD group x = b % 8 takes the contiguous query range
+        // [x*q + min(x, r), ...) so neighbouring (similar) queries share an L2
+        const int nq = p.nq, qd = nq >> 3, rm = nq & 7;
+        const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+        qi = x * qd + min(x, rm) + j;
+    }
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
     WaveLds w = carve(smem, p.ef, false);
@@ -285,7 +292,7 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
     WaveLds w = carve(smem, p.efc, true);
-    const uint32_t node = p.base_slot + (uint32_t)bi;
+    const uint32_t node = p.nodes[bi];
     const int L = p.levels[bi];
     uint64_t ndist = 0, nadj = 0;
     QReg<G, VM, T> q;

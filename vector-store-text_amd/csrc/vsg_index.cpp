@@ -122,6 +122,7 @@ struct vsg_index {
     // build workspace (writer side only)
     int8_t* d_blevels = nullptr;
     uint32_t* d_pair_off = nullptr;
+    uint32_t* d_bnodes = nullptr;
     size_t bnodes_cap = 0;
     uint64_t* d_pk[2] = {nullptr, nullptr};
     uint32_t* d_pv[2] = {nullptr, nullptr};
@@ -159,6 +160,7 @@ static void free_dev(vsg_index* h) {
     hipFree(h->d_stats);
     hipFree(h->d_blevels);
     hipFree(h->d_pair_off);
+    hipFree(h->d_bnodes);
     for (int i = 0; i < 2; ++i) {
         hipFree(h->d_pk[i]);
         hipFree(h->d_pv[i]);
@@ -228,11 +230,14 @@ static int ensure_nodes(vsg_index* h, size_t n) {
     const size_t want = std::max(n, h->bnodes_cap * 2);
     hipFree(h->d_blevels);
     hipFree(h->d_pair_off);
+    hipFree(h->d_bnodes);
     h->d_blevels = nullptr;
     h->d_pair_off = nullptr;
+    h->d_bnodes = nullptr;
     h->bnodes_cap = 0;
     HIP_TRY(dev_alloc(&h->d_blevels, want));
     HIP_TRY(dev_alloc(&h->d_pair_off, want));
+    HIP_TRY(dev_alloc(&h->d_bnodes, want));
     h->bnodes_cap = want;
     return VSG_OK;
 }
@@ -294,28 +299,48 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
     }
 
     if ((rc = ensure_nodes(h, n))) return rc;
-    HIP_TRY(hipMemcpyAsync(h->d_blevels, h->h_levels.data() + s0, n, hipMemcpyHostToDevice, st));
+    // Insertion order = a seeded random permutation of the call's slots: nodes of
+    // one batch cannot link to each other, so a batch must not be spatially
+    // coherent (a cluster-sorted input otherwise wrecks the graph).
+    std::vector<uint32_t> order(n);
+    std::vector<int8_t> blev(n);
+    for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+    {
+        const uint64_t base = host_splitmix64(h->opt.seed ^ 0x5045524D55544Eull ^ (uint64_t)s0);
+        for (size_t i = n; i > 1; --i) {
+            const size_t j = (size_t)(host_splitmix64(base + i) % i);
+            std::swap(order[i - 1], order[j]);
+        }
+    }
+    for (size_t i = 0; i < n; ++i) {
+        order[i] += s0;
+        blev[i] = h->h_levels[order[i]];
+    }
+    HIP_TRY(hipMemcpyAsync(h->d_bnodes, order.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_blevels, blev.data(), n, hipMemcpyHostToDevice, st));
 
     const double frac = env_double("VSG_BUILD_BATCH_FRAC", 1.0 / 16.0);
     const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 32768);
+    // at least 8 batches per call, so the call's own nodes find each other
+    const size_t bcall = std::max<size_t>(1, n / 8);
     std::vector<uint32_t> pair_off(n + 1);
 
     size_t i = 0;
     if (h->entry == 0xFFFFFFFFu) {
-        h->entry = s0;
-        h->max_level = h->h_levels[s0];
+        h->entry = order[0];
+        h->max_level = blev[0];
         i = 1;
     }
     while (i < n) {
-        const size_t graph_nodes = (size_t)s0 + i;
+        const size_t graph_nodes = (size_t)h->slots - n + i;
         size_t b = (size_t)std::floor((double)graph_nodes * frac);
-        b = std::max<size_t>(1, std::min(b, bmax));
+        b = std::max<size_t>(1, std::min(std::min(b, bmax), bcall));
         b = std::min(b, n - i);
         int new_top = -1;
         for (size_t j = i; j < i + b; ++j) {
-            if (h->h_levels[s0 + j] > h->max_level) {
+            if (blev[j] > h->max_level) {
                 b = j - i + 1;
-                new_top = h->h_levels[s0 + j];
+                new_top = blev[j];
                 break;
             }
         }
@@ -323,7 +348,7 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
         uint32_t acc = 0;
         for (size_t j = 0; j < b; ++j) {
             pair_off[i + j] = acc;
-            const int L = std::min<int>(h->h_levels[s0 + i + j], h->max_level);
+            const int L = std::min<int>(blev[i + j], h->max_level);
             acc += (uint32_t)(h->M0 + L * h->M);
         }
         const size_t npairs = acc;
@@ -333,7 +358,7 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
 
         InsertParams ip{};
         ip.g = h->graph();
-        ip.base_slot = s0 + (uint32_t)i;
+        ip.nodes = h->d_bnodes + i;
         ip.nnodes = (int)b;
         ip.levels = h->d_blevels + i;
         ip.pair_off = h->d_pair_off + i;
@@ -366,7 +391,7 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
         HIP_TRY(launch_reverse(h->st, h->mk, rp, grid, st));
 
         if (new_top >= 0) {
-            h->entry = s0 + (uint32_t)(i + b - 1);
+            h->entry = order[i + b - 1];
             h->max_level = new_top;
         }
         h->build_batches++;
@@ -622,6 +647,7 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         p.out_dist = od;
         p.out_counts = oc;
         p.stats = h->d_stats;
+        p.xcd_map = env_double("VSG_SEARCH_XCD_MAP", 0) != 0 ? 1 : 0;
         HIP_TRY(launch_search(h->st, h->mk, p, s));
     } else {
         const size_t slots = h->slots;

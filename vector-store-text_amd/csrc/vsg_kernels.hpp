@@ -31,11 +31,12 @@ struct SearchParams {
     float* out_dist;
     uint32_t* out_counts;
     unsigned long long* stats;  // [0] n_dist, [1] n_adj, [2] queries
+    int xcd_map;                // 1: workgroups b, b+8, ... (one XCD) take consecutive queries
 };
 
 struct InsertParams {
     DevGraph g;
-    uint32_t base_slot;
+    const uint32_t* nodes;     // slots of the batch (insertion order is a random permutation)
     int nnodes;
     const int8_t* levels;      // per batch node
     const uint32_t* pair_off;  // per batch node

@@ -5,10 +5,18 @@ Workload = BASELINE.json configs[1]: 1M x 768 f32, cosine, HNSW M=16, efC=128,
 k=10, clustered-latent synthetic data generated in HBM (vsg/datagen.py formulas).
 One step = one HNSW search pass of the query batch (10,000 queries, inputs
 resident in HBM) at the smallest ef whose recall@10 against exact ground truth is
->= 0.95 (ef swept on a 1,000-query subset).  N > 1: the index is
-row-range sharded (rank r owns rows [r N/G, (r+1) N/G)), every rank searches its
-shard, per-shard top-k is all-gathered over RCCL and k-way merged on every rank
-(SURVEY.md §8e).  Total work is fixed as N grows => "scaling": "strong".
+>= 0.95 (ef swept on a 1,000-query subset).
+
+N > 1 (--multi both, default) measures two legs in one run:
+  * replica (`value`): every rank holds the whole 1M index (3 GB of 288 GB HBM)
+    and serves its own 10,000-query batch per step; per-GPU work fixed =>
+    "scaling": "weak", value = all ranks' queries / max-over-ranks time.
+  * shard (`shard_mode`, the north-star layout): rank r owns rows
+    [r N/G, (r+1) N/G), every query is searched on every shard, per-shard top-k'
+    is all-gathered over RCCL (xGMI) and k-way merged by the HIP merge kernel;
+    (ef, k') re-tuned for merged recall; total work fixed => strong scaling.
+DESIGN.md §6 explains why replicas, not shards, maximise QPS when the index fits
+one GPU, and why shards still win the build.
 
 Also reported: build vectors/s (GPU batched HNSW build of the whole index, max over
 ranks), the HBM roofline of the search kernel (algorithmic bytes counted by the
@@ -59,104 +67,129 @@ def parse():
                     help="experiment: order the query batch by synthetic cluster id")
     ap.add_argument("--sort-base", default="none", choices=("none", "cluster"),
                     help="experiment: insert base rows in synthetic-cluster order (spatial slot ids)")
+    ap.add_argument("--multi", default="both", choices=("both", "shard", "replica"),
+                    help="N>1: row-range shards + all-gather merge (strong) and/or full replicas + query "
+                         "split (weak); 'both' reports replica QPS as value and the shard leg beside it")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse several ranks on one GPU (collectives via host)")
     return ap.parse_args()
 
 
-def main():
-    a = parse()
+class Ctx:
+    """Per-process run context (rank, device, collectives)."""
+
+    def __init__(self, a):
+        import torch
+        import torch.distributed as dist
+
+        self.a = a
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.local = local % max(1, torch.cuda.device_count())  # >1 rank per GPU only for gloo rehearsal
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+        if self.world > 1:
+            if a.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(a.dist_backend)
+        self.stream = torch.cuda.current_stream()
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def max_over_ranks(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        dev = self.dev if self.a.dist_backend == "nccl" else "cpu"
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def hnsw_leg(c, mode):
+    """One HNSW measurement.  mode: "single" (N=1), "shard" (row-range shards,
+    every query on every shard, RCCL all-gather + HIP merge; strong scaling) or
+    "replica" (every rank holds the whole index and serves its own query batch;
+    weak scaling).  Returns the measured fields and the index."""
+    import numpy as np
     import torch
-    import torch.distributed as dist
 
     import vsg
     from vsg import datagen as G
-
     from vsg.distributed import gather_topk, merge_topk
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    local = local % max(1, torch.cuda.device_count())  # >1 rank per GPU only for gloo rehearsal
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(a.dist_backend)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    def max_over_ranks(x: float) -> float:
-        if world == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
+    a, world, rank = c.a, c.world, c.rank
+    sharded = mode == "shard"
+    replica = mode == "replica"
     bs, qs, ms = G.config_seeds(a.config)
-    lo, hi = rank * a.rows // world, (rank + 1) * a.rows // world
+    lo, hi = (rank * a.rows // world, (rank + 1) * a.rows // world) if sharded else (0, a.rows)
     nloc = hi - lo
-    stream = torch.cuda.current_stream()
 
-    # ---- inputs in HBM
+    # inputs in HBM
     x = vsg.datagen_device("clustered", nloc, a.dim, bs, ms, start=lo)
-    q = vsg.datagen_device("clustered", a.queries, a.dim, qs, ms)
+    q = vsg.datagen_device("clustered", a.queries, a.dim, qs, ms, start=(rank * a.queries if replica else 0))
+    qgt = vsg.datagen_device("clustered", a.gt_queries, a.dim, qs, ms, start=0)  # same on every rank
     if a.sort_queries == "cluster":
         cl = (G.splitmix64(G._stream(qs, G.TAG_CLUSTER) + np.arange(a.queries, dtype=np.uint64))
               % np.uint64(G.N_CENTRES)).astype(np.int64)
-        q = q[torch.from_numpy(np.argsort(cl, kind="stable")).to(dev)].contiguous()
-    torch.cuda.synchronize()
-
-    if a.mode == "exact":
-        return run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_over_ranks)
-
-    # ---- build (timed; not part of the QPS step)
-    index = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 128, device=local, seed=0x5EED + rank)
-    index.reserve(nloc)
+        q = q[torch.from_numpy(np.argsort(cl, kind="stable")).to(c.dev)].contiguous()
     keys_np = np.arange(lo, hi, dtype=np.uint64)
     if a.sort_base == "cluster":
         cl = (G.splitmix64(G._stream(bs, G.TAG_CLUSTER) + keys_np) % np.uint64(G.N_CENTRES)).astype(np.int64)
         order = np.argsort(cl, kind="stable")
-        x = x[torch.from_numpy(order).to(dev)].contiguous()
+        x = x[torch.from_numpy(order).to(c.dev)].contiguous()
         keys_np = keys_np[order]
-    barrier()
-    t0 = time.perf_counter()
-    index.add_device(keys_np, x, stream=stream)
     torch.cuda.synchronize()
-    build_s = max_over_ranks(time.perf_counter() - t0)
-    build_vps = a.rows / build_s
+
+    # build (timed; not part of the QPS step)
+    seed = 0x5EED + (rank if sharded else 0)
+    index = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 128, device=c.local, seed=seed)
+    index.reserve(nloc)
+    c.barrier()
+    t0 = time.perf_counter()
+    index.add_device(keys_np, x, stream=c.stream)
+    torch.cuda.synchronize()
+    build_s = c.max_over_ranks(time.perf_counter() - t0)
+    rows_built = a.rows if sharded else a.rows  # sharded: N shards of rows/N concurrently
     bstats = index.stats()
 
-    def sharded(qt, ef, exact=False):
-        keys, dists = index.search_device(qt, a.k, ef, stream=stream, exact=exact)
-        if world == 1:
+    def search(qt, ef, ks, exact=False):
+        keys, dists = index.search_device(qt, ks, ef, stream=c.stream, exact=exact)
+        if not sharded:
             return keys, dists
         gk, gd = gather_topk(keys, dists)
-        return merge_topk(gk, gd, a.k, stream=stream)
+        return merge_topk(gk, gd, a.k, stream=c.stream)
 
-    # ---- ground truth (exact, GPU brute force, same sharded merge path)
-    qgt = q[: a.gt_queries].contiguous()
-    gt_keys, _ = sharded(qgt, 0, exact=True)
-    gt = gt_keys.cpu().numpy()
+    # ground truth: exact GPU brute force (f32 MFMA), same merge path
+    gt = search(qgt, 0, a.k, exact=True)[0].cpu().numpy()
 
     def recall_of(keys_t):
         f = keys_t.cpu().numpy()
         return float(np.mean([len(set(f[i]) & set(gt[i])) / a.k for i in range(gt.shape[0])]))
 
-    # ---- ef selection
+    # (ef, k_shard): smallest ef whose merged recall@k >= target.  A shard returns
+    # k_shard = min(k, ef) candidates (shards x k_shard >= k); one index returns k.
+    def kshard(ef):
+        return min(a.k, ef) if sharded else a.k
+
     sweep = []
     if a.ef:
         ef = a.ef
-        sweep.append((ef, recall_of(sharded(qgt, ef)[0])))
+        sweep.append((ef, recall_of(search(qgt, ef, kshard(ef))[0])))
     else:
+        grid = (4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512)
+        if not sharded:
+            grid = tuple(e for e in grid if e >= max(16, a.k))
         ef, lo_fail = None, None
-        for cand in (16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512):
-            r = recall_of(sharded(qgt, cand)[0])
+        for cand in grid:
+            if sharded and cand * world < a.k:
+                continue
+            r = recall_of(search(qgt, cand, kshard(cand))[0])
             sweep.append((cand, r))
             if r >= a.target_recall:
                 ef = cand
@@ -165,11 +198,10 @@ def main():
         if ef is None:
             ef = sweep[-1][0]
         elif lo_fail is not None:
-            # smallest ef in (lo_fail, ef] that still meets the target
             e_lo, e_hi = lo_fail, ef
-            while e_hi - e_lo > 2:
+            while e_hi - e_lo > 1:
                 mid = (e_lo + e_hi) // 2
-                r = recall_of(sharded(qgt, mid)[0])
+                r = recall_of(search(qgt, mid, kshard(mid))[0])
                 sweep.append((mid, r))
                 if r >= a.target_recall:
                     e_hi = mid
@@ -177,74 +209,126 @@ def main():
                     e_lo = mid
             ef = e_hi
     recall = dict(sweep)[ef]
+    ks = kshard(ef)
 
-    # ---- timed QPS steps
+    # timed QPS steps: W warmup, then exactly K steps between barriers
     for _ in range(a.warmup):
-        sharded(q, ef)
+        search(q, ef, ks)
     index.reset_stats()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     kern_ms = 0.0
-    barrier()
+    c.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        ev0.record(stream)
-        keys, dists = index.search_device(q, a.k, ef, stream=stream)
-        ev1.record(stream)
-        if world > 1:
+        ev0.record(c.stream)
+        keys, dists = index.search_device(q, ks, ef, stream=c.stream)
+        ev1.record(c.stream)
+        if sharded:
             gk, gd = gather_topk(keys, dists)
-            keys, dists = merge_topk(gk, gd, a.k, stream=stream)
+            keys, dists = merge_topk(gk, gd, a.k, stream=c.stream)
         torch.cuda.synchronize()
         kern_ms += ev0.elapsed_time(ev1)
-    barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
-    ms_per_step = 1000.0 * elapsed / a.steps
-    qps = a.queries * a.steps / elapsed
+    c.barrier()
+    elapsed = c.max_over_ranks(time.perf_counter() - t0)
+    queries_done = (world if replica else 1) * a.queries * a.steps
     st = index.stats()
     per16 = 4 if a.quant == "f32" else 8
     row_bytes = ((a.dim + per16 - 1) // per16) * 16
     alg_bytes = (st["search_distances"] * row_bytes + st["search_adjacency"] * 2 * a.M * 4) / a.steps
     kern_ms_avg = kern_ms / a.steps
-    achieved = alg_bytes / (kern_ms_avg * 1e-3) / 1e9
+    return {
+        "mode": mode, "index": index, "q": q, "x": x, "nloc": nloc,
+        "qps": queries_done / elapsed, "ms_per_step": 1000.0 * elapsed / a.steps,
+        "ef": ef, "k_shard": ks, "recall": recall, "sweep": sweep,
+        "build_s": build_s, "build_vps": rows_built / build_s,
+        "kern_ms": kern_ms_avg, "alg_bytes": alg_bytes,
+        "achieved_gbs": alg_bytes / (kern_ms_avg * 1e-3) / 1e9,
+        "dist_per_query": st["search_distances"] / max(1, st["search_queries"]),
+        "build_dist_per_vector": bstats["build_distances"] / max(1, nloc),
+        "build_batches": bstats["build_batches"],
+    }
 
+
+def main():
+    a = parse()
+    c = Ctx(a)
+    world, rank = c.world, c.rank
+    if a.mode == "exact":
+        import vsg
+        from vsg import datagen as G
+        bs, qs, ms = G.config_seeds(a.config)
+        lo, hi = rank * a.rows // world, (rank + 1) * a.rows // world
+        x = vsg.datagen_device("clustered", hi - lo, a.dim, bs, ms, start=lo)
+        q = vsg.datagen_device("clustered", a.batch, a.dim, qs, ms)
+        run_exact(a, x, q, lo, hi, world, rank, c.local, c.dev, c.stream, c.barrier, c.max_over_ranks)
+        if world > 1:
+            c.dist.destroy_process_group()
+        return
+
+    if world == 1:
+        legs = ["single"]
+    else:
+        legs = ["shard", "replica"] if a.multi == "both" else [a.multi]
+    res = {}
+    for m in legs:
+        if res:  # free the previous leg's HBM before the next build
+            res[list(res)[-1]].pop("index", None)
+        res[m] = hnsw_leg(c, m)
+    head = res["replica"] if "replica" in res else res[legs[0]]
+    replica = head["mode"] == "replica"
     out = {
-        "metric": "kNN QPS @ recall@10>=0.95 (HNSW, 1M x 768 f32 cos)",
-        "value": round(qps, 1),
+        "metric": f"kNN QPS @ recall@10>={a.target_recall} (HNSW, {a.rows} x {a.dim} {a.quant} {a.metric})",
+        "value": round(head["qps"], 1),
         "unit": "queries/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(ms_per_step, 3),
+        "ms_per_step": round(head["ms_per_step"], 3),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if replica else "strong",
         "vs_baseline": None,
         "dtype": a.quant,
-        "data": "synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py), 10k queries/step",
+        "data": f"synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py), "
+                f"{a.queries} queries/step" + ("/GPU" if replica else ""),
         "config": {"workload": f"C2: {a.rows} x {a.dim} f32 {a.metric} HNSW M={a.M} efC={a.efc} k={a.k}",
-                   "index_rows": a.rows, "dim": a.dim, "queries_per_step": a.queries,
-                   "ef": ef, "recall_at_10": round(recall, 4), "ef_sweep": sweep,
-                   "parallelism": f"row-shard x{world}" + (" + RCCL all-gather top-k" if world > 1 else "")},
-        "build_vectors_per_s": round(build_vps, 1),
-        "build_seconds": round(build_s, 3),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic(a, ef),
-                     "kernel": "hnsw_search_kernel<64,3,4,float,1>", "kernel_ms": round(kern_ms_avg, 3),
-                     "alg_bytes_per_launch": int(alg_bytes),
-                     "dist_evals_per_query": round(st["search_distances"] / max(1, st["search_queries"]), 1)},
-        "build_stats": {"distance_evals_per_vector": round(bstats["build_distances"] / max(1, nloc), 1),
-                        "batches": bstats["build_batches"]},
+                   "index_rows": a.rows, "dim": a.dim, "queries_per_step": a.queries * (world if replica else 1),
+                   "ef": head["ef"], "k_shard": head["k_shard"], "recall_at_10": round(head["recall"], 4),
+                   "ef_sweep": head["sweep"],
+                   "parallelism": {"single": "1 GPU",
+                                   "shard": f"row-shard x{world} + RCCL all-gather top-k + HIP merge",
+                                   "replica": f"replica x{world}, query split ({a.queries} queries/GPU/step)"}[
+                                       head["mode"]]},
+        "build_vectors_per_s": round(head["build_vps"], 1),
+        "build_seconds": round(head["build_s"], 3),
+        "roofline": {"bound": "hbm", "achieved": round(head["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(head["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic(a, head["ef"]) if head["mode"] != "shard" else None,
+                     "kernel": "hnsw_search_kernel", "kernel_ms": round(head["kern_ms"], 3),
+                     "alg_bytes_per_launch": int(head["alg_bytes"]),
+                     "dist_evals_per_query": round(head["dist_per_query"], 1)},
+        "build_stats": {"distance_evals_per_vector": round(head["build_dist_per_vector"], 1),
+                        "batches": head["build_batches"]},
     }
-
-    # ---- CPU baseline (rank 0, N=1 only): oracle/ restatement of usearch
+    if "shard" in res and head["mode"] != "shard":
+        s = res["shard"]
+        out["shard_mode"] = {"qps": round(s["qps"], 1), "ms_per_step": round(s["ms_per_step"], 3),
+                             "ef": s["ef"], "k_shard": s["k_shard"], "recall_at_10": round(s["recall"], 4),
+                             "build_vectors_per_s": round(s["build_vps"], 1),
+                             "build_seconds": round(s["build_s"], 3),
+                             "kernel_ms": round(s["kern_ms"], 3),
+                             "dist_evals_per_query_per_shard": round(s["dist_per_query"], 1),
+                             "scaling": "strong", "note": "row-range shards, every query searched on every shard"}
+    # CPU baseline (rank 0, N=1 only): oracle/ restatement of usearch
     if world == 1 and rank == 0 and not a.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(a, index, q, ef, x)
+        out["cpu_baseline"] = cpu_baseline(a, head["index"], head["q"], head["ef"], head["x"])
         if out["cpu_baseline"].get("qps"):
-            out["gpu_over_cpu_qps"] = round(qps / out["cpu_baseline"]["qps"], 1)
+            out["gpu_over_cpu_qps"] = round(head["qps"] / out["cpu_baseline"]["qps"], 1)
+            out["gpu_over_cpu_build"] = round(head["build_vps"] / out["cpu_baseline"]["build_vectors_per_s"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        c.dist.destroy_process_group()
 
 
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense

@@ -132,10 +132,12 @@ int vsg_index_exact_search_device(vsg_index_t* index, const float* queries_devic
                                   void* stream);
 
 /* k-way merge of per-shard top-k rows (after an all-gather over xGMI,
- * SURVEY §8e): parts x nq x k (keys, distances) -> nq x k ascending. */
+ * SURVEY §8e): parts x nq x k_in (keys, distances; rows ascending, padded with
+ * VSG_NO_KEY) -> nq x k_out ascending by (distance, key).  k_in < k_out is
+ * allowed: a shard may return fewer candidates than the final k. */
 int vsg_merge_topk_device(const uint64_t* keys_device, const float* distances_device,
-                          size_t parts, size_t nq, size_t k, uint64_t* out_keys_device,
-                          float* out_distances_device, void* stream);
+                          size_t parts, size_t nq, size_t k_in, size_t k_out,
+                          uint64_t* out_keys_device, float* out_distances_device, void* stream);
 
 int vsg_index_stats(const vsg_index_t* index, vsg_stats_t* out);
 int vsg_index_reset_stats(vsg_index_t* index);

@@ -65,6 +65,19 @@ def test_sharded_merge_matches_single_index(tmp_path, world, metric):
         np.testing.assert_array_equal(md, od)
 
 
+def test_merge_topk_cpu_short_shards():
+    """Shards may return k_shard < k candidates (bench sweeps (ef, k_shard))."""
+    sys.path.insert(0, os.path.join(ROOT, "vector-store-text_amd"))
+    from vsg.distributed import merge_topk
+
+    gk = torch.tensor([[[1, 4]], [[2, 3]], [[7, -1]]], dtype=torch.int64)
+    gd = torch.tensor([[[0.1, 0.4]], [[0.2, 0.3]], [[0.05, float("inf")]]])
+    mk, md = merge_topk(gk, gd, 4)
+    assert mk.tolist() == [[7, 1, 2, 3]]
+    mk, md = merge_topk(gk[:1], gd[:1], 3)  # fewer candidates than k: padded
+    assert mk.tolist() == [[1, 4, -1]] and md[0, 2] == float("inf")
+
+
 def test_merge_topk_cpu_padding_and_ties():
     sys.path.insert(0, os.path.join(ROOT, "vector-store-text_amd"))
     from vsg.distributed import merge_topk

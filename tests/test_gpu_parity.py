@@ -341,6 +341,12 @@ def test_device_api_and_shard_merge():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(mk.cpu().numpy().astype(np.uint64), truth.keys)
     np.testing.assert_array_equal(md.cpu().numpy(), truth.distances)
+    # shorter shard lists (k_shard = 6 < k): HIP merge == host merge
+    from vsg.distributed import merge_topk
+    mk2, md2 = vsg.merge_topk_device(keys[:, :, :6].contiguous(), dist[:, :, :6].contiguous(), 10)
+    hk, hd = merge_topk(keys[:, :, :6].cpu(), dist[:, :, :6].cpu(), 10)
+    np.testing.assert_array_equal(mk2.cpu().numpy(), hk.numpy())
+    np.testing.assert_array_equal(md2.cpu().numpy(), hd.numpy())
 
 
 def test_datagen_device_matches_numpy():

@@ -124,22 +124,23 @@ hipError_t launch_merge_parts(const MergeParams& p, hipStream_t s) {
 }
 
 // k-way merge of sorted per-shard rows: one thread per query, (distance, key)
-// order.  parts x nq x k inputs (all-gathered shard results).
+// order.  parts x nq x k_in inputs (all-gathered shard results, SURVEY §8e;
+// a shard may return fewer candidates than the final k) -> nq x k_out.
 __global__ void merge_topk64_kernel(const uint64_t* __restrict__ keys, const float* __restrict__ dist,
-                                    int parts, int nq, int k, uint64_t* __restrict__ out_keys,
+                                    int parts, int nq, int kin, int kout, uint64_t* __restrict__ out_keys,
                                     float* __restrict__ out_dist) {
     const int qi = blockIdx.x * blockDim.x + threadIdx.x;
     if (qi >= nq) return;
     int ptr[64];
     const int P = parts < 64 ? parts : 64;
     for (int pp = 0; pp < P; ++pp) ptr[pp] = 0;
-    for (int j = 0; j < k; ++j) {
+    for (int j = 0; j < kout; ++j) {
         int best = -1;
         float bd = __builtin_inff();
         uint64_t bk = ~0ull;
         for (int pp = 0; pp < P; ++pp) {
-            if (ptr[pp] >= k) continue;
-            const size_t o = ((size_t)pp * nq + qi) * k + ptr[pp];
+            if (ptr[pp] >= kin) continue;
+            const size_t o = ((size_t)pp * nq + qi) * kin + ptr[pp];
             const uint64_t kk = keys[o];
             if (kk == ~0ull) continue;
             const float dd = dist[o];
@@ -149,17 +150,17 @@ __global__ void merge_topk64_kernel(const uint64_t* __restrict__ keys, const flo
                 bk = kk;
             }
         }
-        out_keys[(size_t)qi * k + j] = best < 0 ? ~0ull : bk;
-        out_dist[(size_t)qi * k + j] = best < 0 ? __builtin_inff() : bd;
+        out_keys[(size_t)qi * kout + j] = best < 0 ? ~0ull : bk;
+        out_dist[(size_t)qi * kout + j] = best < 0 ? __builtin_inff() : bd;
         if (best >= 0) ptr[best]++;
     }
 }
 
-hipError_t launch_merge_topk64(const uint64_t* keys, const float* dist, int parts, int nq, int k,
+hipError_t launch_merge_topk64(const uint64_t* keys, const float* dist, int parts, int nq, int kin, int kout,
                                uint64_t* out_keys, float* out_dist, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(merge_topk64_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, keys, dist, parts, nq, k,
-                       out_keys, out_dist);
+    hipLaunchKernelGGL(merge_topk64_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, keys, dist, parts, nq, kin,
+                       kout, out_keys, out_dist);
     return hipGetLastError();
 }
 

@@ -770,10 +770,12 @@ int vsg_index_exact_search_device(vsg_index_t* h, const float* q, size_t nq, siz
     return search_device_locked(h, q, nq, k, 0, ok, od, oc, (hipStream_t)stream, true);
 }
 
-int vsg_merge_topk_device(const uint64_t* keys, const float* dist, size_t parts, size_t nq, size_t k,
-                          uint64_t* out_keys, float* out_dist, void* stream) {
+int vsg_merge_topk_device(const uint64_t* keys, const float* dist, size_t parts, size_t nq, size_t k_in,
+                          size_t k_out, uint64_t* out_keys, float* out_dist, void* stream) {
     if (parts == 0 || parts > 64) return fail(VSG_EINVAL, "parts must be in [1, 64]");
-    HIP_TRY(launch_merge_topk64(keys, dist, (int)parts, (int)nq, (int)k, out_keys, out_dist, (hipStream_t)stream));
+    if (k_in == 0 || k_out == 0) return fail(VSG_EINVAL, "k must be >= 1");
+    HIP_TRY(launch_merge_topk64(keys, dist, (int)parts, (int)nq, (int)k_in, (int)k_out, out_keys, out_dist,
+                                (hipStream_t)stream));
     return VSG_OK;
 }
 

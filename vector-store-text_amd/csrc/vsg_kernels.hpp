@@ -118,7 +118,7 @@ hipError_t launch_merge_parts(const MergeParams& p, hipStream_t s);
 // returns hipErrorNotSupported when the MFMA path does not apply (k > 32)
 hipError_t launch_mfma_exact(MetricKind mk, const MfmaExactParams& p, hipStream_t s);
 constexpr int MFMA_BQ = 128, MFMA_BR = 128;
-hipError_t launch_merge_topk64(const uint64_t* keys, const float* dist, int parts, int nq, int k,
+hipError_t launch_merge_topk64(const uint64_t* keys, const float* dist, int parts, int nq, int kin, int kout,
                                uint64_t* out_keys, float* out_dist, hipStream_t s);
 // f32 rows (stride dim) -> storage rows (row_bytes), normalised when `normalize`
 hipError_t launch_prepare(Storage st, const float* in, size_t n, int dim, bool normalize,

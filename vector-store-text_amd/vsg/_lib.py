@@ -103,7 +103,7 @@ def lib() -> C.CDLL:
         "vsg_index_exact_search": (C.c_int, [P, P, sz, sz, P, P, P]),
         "vsg_index_search_device": (C.c_int, [P, P, sz, sz, sz, P, P, P, P]),
         "vsg_index_exact_search_device": (C.c_int, [P, P, sz, sz, P, P, P, P]),
-        "vsg_merge_topk_device": (C.c_int, [P, P, sz, sz, sz, P, P, P]),
+        "vsg_merge_topk_device": (C.c_int, [P, P, sz, sz, sz, sz, P, P, P]),
         "vsg_index_stats": (C.c_int, [P, C.POINTER(Stats)]),
         "vsg_index_reset_stats": (C.c_int, [P]),
         "vsg_index_graph_info": (C.c_int, [P, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz),

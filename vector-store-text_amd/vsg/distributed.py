@@ -48,6 +48,9 @@ def merge_topk(gk: torch.Tensor, gd: torch.Tensor, k: int, stream=None):
     parts, nq, kk = gk.shape
     keys = gk.permute(1, 0, 2).reshape(nq, parts * kk)
     d = gd.permute(1, 0, 2).reshape(nq, parts * kk).clone()
+    if parts * kk < k:  # shards returned fewer candidates than k: pad
+        keys = torch.cat([keys, torch.full((nq, k - parts * kk), -1, dtype=keys.dtype)], 1)
+        d = torch.cat([d, torch.full((nq, k - parts * kk), float("inf"), dtype=d.dtype)], 1)
     pad = keys == -1
     d[pad] = float("inf")
     # lexicographic (distance, key): stable sort by key (as unsigned), then by distance
@@ -60,9 +63,12 @@ def merge_topk(gk: torch.Tensor, gd: torch.Tensor, k: int, stream=None):
 
 
 def sharded_search(index, queries: torch.Tensor, k: int, ef: int = 0, exact: bool = False,
-                   group=None, stream=None):
-    """Search every shard, gather, merge.  `index` is this rank's vsg.Index."""
-    keys, dists = index.search_device(queries, k, ef, stream=stream, exact=exact)
+                   group=None, stream=None, k_shard: int = 0):
+    """Search every shard, gather, merge.  `index` is this rank's vsg.Index.
+    k_shard (<= k) candidates per shard suffice when the merged recall target
+    allows it (each shard holds ~1/G of the true neighbours)."""
+    ks = k_shard or k
+    keys, dists = index.search_device(queries, ks, ef, stream=stream, exact=exact)
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return keys, dists
     gk, gd = gather_topk(keys, dists, group)

@@ -186,13 +186,12 @@ class Index:
 
 
 def merge_topk_device(keys_t, dist_t, k, stream=None):
-    """k-way merge of gathered per-shard results: (parts, nq, k) -> (nq, k)."""
+    """k-way merge of gathered per-shard results: (parts, nq, k_in) -> (nq, k)."""
     import torch
-    parts, nq, kk = keys_t.shape
-    assert kk == k
+    parts, nq, kin = keys_t.shape
     ok = torch.empty((nq, k), dtype=torch.int64, device=keys_t.device)
     od = torch.empty((nq, k), dtype=torch.float32, device=keys_t.device)
-    check(lib().vsg_merge_topk_device(_tp(keys_t), _tp(dist_t), parts, nq, k, _tp(ok), _tp(od),
+    check(lib().vsg_merge_topk_device(_tp(keys_t), _tp(dist_t), parts, nq, kin, k, _tp(ok), _tp(od),
                                       _stream_ptr(stream)))
     return ok, od
 

@@ -63,6 +63,8 @@ def parse():
                     help="exact: brute-force MFMA path (C5: --rows 1000000 --dim 1536 --metric ip)")
     ap.add_argument("--batch", type=int, default=1024, help="exact mode: queries per step")
     ap.add_argument("--quant", default="f32", choices=("f32", "f16"), help="HBM storage type")
+    ap.add_argument("--data", default="clustered", choices=("clustered", "sift", "gaussian"),
+                    help="synthetic generator (sift: clustered, ReLU, x48, rounded 0..255; C4)")
     ap.add_argument("--sort-queries", default="none", choices=("none", "cluster"),
                     help="experiment: order the query batch by synthetic cluster id")
     ap.add_argument("--sort-base", default="none", choices=("none", "cluster"),
@@ -131,9 +133,9 @@ def hnsw_leg(c, mode):
     nloc = hi - lo
 
     # inputs in HBM
-    x = vsg.datagen_device("clustered", nloc, a.dim, bs, ms, start=lo)
-    q = vsg.datagen_device("clustered", a.queries, a.dim, qs, ms, start=(rank * a.queries if replica else 0))
-    qgt = vsg.datagen_device("clustered", a.gt_queries, a.dim, qs, ms, start=0)  # same on every rank
+    x = vsg.datagen_device(a.data, nloc, a.dim, bs, ms, start=lo)
+    q = vsg.datagen_device(a.data, a.queries, a.dim, qs, ms, start=(rank * a.queries if replica else 0))
+    qgt = vsg.datagen_device(a.data, a.gt_queries, a.dim, qs, ms, start=0)  # same on every rank
     if a.sort_queries == "cluster":
         cl = (G.splitmix64(G._stream(qs, G.TAG_CLUSTER) + np.arange(a.queries, dtype=np.uint64))
               % np.uint64(G.N_CENTRES)).astype(np.int64)
@@ -291,7 +293,8 @@ def main():
         "dtype": a.quant,
         "data": f"synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py), "
                 f"{a.queries} queries/step" + ("/GPU" if replica else ""),
-        "config": {"workload": f"C2: {a.rows} x {a.dim} f32 {a.metric} HNSW M={a.M} efC={a.efc} k={a.k}",
+        "config": {"workload": f"C{a.config + 1}: {a.rows} x {a.dim} {a.data} f32 input, {a.quant} storage, "
+                               f"{a.metric} HNSW M={a.M} efC={a.efc} k={a.k}",
                    "index_rows": a.rows, "dim": a.dim, "queries_per_step": a.queries * (world if replica else 1),
                    "ef": head["ef"], "k_shard": head["k_shard"], "recall_at_10": round(head["recall"], 4),
                    "ef_sweep": head["sweep"],

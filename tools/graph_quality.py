@@ -25,15 +25,18 @@ def main():
     ap.add_argument("--metric", default="cos")
     ap.add_argument("--queries", type=int, default=1000)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--data", default="clustered")
+    ap.add_argument("--config", type=int, default=1)
+    ap.add_argument("--efs", default="16,24,32,36,48,64,128")
     a = ap.parse_args()
     import torch
     import oracle as O
     import vsg
     from vsg import datagen as G
 
-    bs, qs, ms = G.config_seeds(1)
-    x = vsg.datagen_device("clustered", a.rows, a.dim, bs, ms)
-    q = vsg.datagen_device("clustered", a.queries, a.dim, qs, ms)
+    bs, qs, ms = G.config_seeds(a.config)
+    x = vsg.datagen_device(a.data, a.rows, a.dim, bs, ms)
+    q = vsg.datagen_device(a.data, a.queries, a.dim, qs, ms)
     idx = vsg.Index(a.dim, a.metric, "f32", 16, 128, 64, seed=1)
     t0 = time.time()
     idx.add_device(np.arange(a.rows, dtype=np.uint64), x)
@@ -48,15 +51,21 @@ def main():
     t0 = time.time()
     hc.add(np.arange(a.rows), xh, threads=a.threads)
     cpu_build = time.time() - t0
-    res = {"rows": a.rows, "gpu_build_s": round(gpu_build, 2), "cpu_build_s": round(cpu_build, 2),
+    res = {"rows": a.rows, "dim": a.dim, "data": a.data, "metric": a.metric,
+           "gpu_build_s": round(gpu_build, 2), "cpu_build_s": round(cpu_build, 2),
            "cpu_threads": a.threads, "recall": {}}
-    for ef in (16, 24, 32, 36, 48, 64, 128):
+    # the CPU-built graph searched by the GPU kernel too
+    ic = vsg.Index(a.dim, a.metric, "f32", 16, 128, 64, seed=1)
+    ic.import_graph(hc.export())
+    for ef in [int(e) for e in a.efs.split(",")]:
         rg = np.mean([len(set(r) & set(t)) / 10 for r, t in zip(hg.search(qh, 10, ef)[0], gt)])
         rc = np.mean([len(set(r) & set(t)) / 10 for r, t in zip(hc.search(qh, 10, ef)[0], gt)])
         kg = idx.search(qh, 10, ef).keys
         rk = np.mean([len(set(r) & set(t)) / 10 for r, t in zip(kg, gt)])
+        kc = ic.search(qh, 10, ef).keys
+        rkc = np.mean([len(set(r) & set(t)) / 10 for r, t in zip(kc, gt)])
         res["recall"][ef] = {"gpu_graph_cpu_search": round(rg, 4), "cpu_graph_cpu_search": round(rc, 4),
-                             "gpu_graph_gpu_search": round(rk, 4)}
+                             "gpu_graph_gpu_search": round(rk, 4), "cpu_graph_gpu_search": round(rkc, 4)}
     print(json.dumps(res))
 
 

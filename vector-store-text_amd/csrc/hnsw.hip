@@ -426,8 +426,18 @@ hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipSt
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(hnsw_search_kernel, sh, tt, mt);
         if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(kern, dim3(p.nq), dim3(64), lds, s, p);
-        err = hipGetLastError();
+        // <= 4M queries per dispatch (64 work-items each: the AQL grid size is 32-bit)
+        constexpr int CH = 1 << 22;
+        for (int off = 0; off < p.nq && err == hipSuccess; off += CH) {
+            SearchParams c = p;
+            c.nq = min(CH, p.nq - off);
+            c.queries = p.queries + (size_t)off * p.g.row_bytes;
+            c.out_keys = p.out_keys + (size_t)off * p.k;
+            c.out_dist = p.out_dist + (size_t)off * p.k;
+            c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
+            hipLaunchKernelGGL(kern, dim3(c.nq), dim3(64), lds, s, c);
+            err = hipGetLastError();
+        }
     });
     return err;
 }

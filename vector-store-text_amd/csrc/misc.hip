@@ -1,5 +1,9 @@
 // misc.hip — row preparation (f32 -> storage type, cos normalisation),
 // tombstone scatter and the HBM synthetic-data generator.
+//
+// Every kernel here walks its rows / elements with a grid-stride loop over a
+// capped grid: the AQL dispatch packet counts work-items in 32 bits, so a
+// one-wave-per-row launch overflows beyond 2^32 / 64 = 67M rows (C4 is 100M).
 #include <hip/hip_runtime.h>
 
 #include "vsg_device.hpp"
@@ -7,55 +11,64 @@
 
 namespace vsg {
 
+// blocks for `items` work units of `per_block` each, capped well below the 2^32
+// work-item limit of one dispatch (kernels loop over the remainder)
+static inline unsigned capped_grid(size_t items, size_t per_block, size_t cap = 1u << 20) {
+    size_t g = (items + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    return (unsigned)(g < cap ? g : cap);
+}
+
 // One wave per row.  Cos rows are stored unit-normalised (x / |x|) so the
 // traversal kernels evaluate cos as 1 - dot.
 template <typename T>
 __global__ __launch_bounds__(256) void prepare_kernel(const float* __restrict__ in, size_t n, int dim,
                                                       int normalize, uint8_t* __restrict__ out,
                                                       size_t row_bytes, float* __restrict__ sqnorm) {
-    const size_t row = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (row >= n) return;
-    const float* x = in + row * (size_t)dim;
-    T* y = reinterpret_cast<T*>(out + row * row_bytes);
-    float nrm = 1.f;
-    if (normalize) {
-        float s = 0.f;
-        for (int j = lane; j < dim; j += 64) s += x[j] * x[j];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-        nrm = sqrtf(s);
-    }
     const int padded = (int)(row_bytes / sizeof(T));
-    float s2 = 0.f;
-    for (int j = lane; j < padded; j += 64) {
-        float v = 0.f;
-        if (j < dim) v = (normalize && nrm > 0.f) ? x[j] / nrm : (normalize ? 0.f : x[j]);
-        const T t = (T)v;
-        y[j] = t;
-        s2 += (float)t * (float)t;
-    }
-    if (sqnorm) {  // |stored row|^2 for the MFMA L2 expansion |x|^2 + |q|^2 - 2 x.q
+    for (size_t row = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (size_t)gridDim.x * 4) {
+        const float* x = in + row * (size_t)dim;
+        T* y = reinterpret_cast<T*>(out + row * row_bytes);
+        float nrm = 1.f;
+        if (normalize) {
+            float s = 0.f;
+            for (int j = lane; j < dim; j += 64) s += x[j] * x[j];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
-        if (lane == 0) sqnorm[row] = s2;
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            nrm = sqrtf(s);
+        }
+        float s2 = 0.f;
+        for (int j = lane; j < padded; j += 64) {
+            float v = 0.f;
+            if (j < dim) v = (normalize && nrm > 0.f) ? x[j] / nrm : (normalize ? 0.f : x[j]);
+            const T t = (T)v;
+            y[j] = t;
+            s2 += (float)t * (float)t;
+        }
+        if (sqnorm) {  // |stored row|^2 for the MFMA L2 expansion |x|^2 + |q|^2 - 2 x.q
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+            if (lane == 0) sqnorm[row] = s2;
+        }
     }
 }
 
 template <typename T>
 __global__ void unprepare_kernel(const uint8_t* __restrict__ in, size_t n, int dim, size_t row_bytes,
                                  float* __restrict__ out) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n * (size_t)dim) return;
-    const size_t r = i / dim;
-    const int j = (int)(i % dim);
-    out[i] = (float)reinterpret_cast<const T*>(in + r * row_bytes)[j];
+    const size_t tot = n * (size_t)dim;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / dim;
+        const int j = (int)(i % dim);
+        out[i] = (float)reinterpret_cast<const T*>(in + r * row_bytes)[j];
+    }
 }
 
 hipError_t launch_prepare(Storage st, const float* in, size_t n, int dim, bool normalize, uint8_t* out,
                           size_t row_bytes, hipStream_t s, float* sqnorm) {
     if (n == 0) return hipSuccess;
-    const dim3 grid((unsigned)((n + 3) / 4));
+    const dim3 grid(capped_grid(n, 4));
     if (st == ST_F32)
         hipLaunchKernelGGL(prepare_kernel<float>, grid, dim3(256), 0, s, in, n, dim, normalize ? 1 : 0, out, row_bytes,
                            sqnorm);
@@ -69,7 +82,7 @@ hipError_t launch_unprepare(Storage st, const uint8_t* in, size_t n, int dim, si
                             hipStream_t s) {
     const size_t tot = n * (size_t)dim;
     if (tot == 0) return hipSuccess;
-    const dim3 grid((unsigned)((tot + 255) / 256));
+    const dim3 grid(capped_grid(tot, 256));
     if (st == ST_F32)
         hipLaunchKernelGGL(unprepare_kernel<float>, grid, dim3(256), 0, s, in, n, dim, row_bytes, out);
     else
@@ -78,14 +91,13 @@ hipError_t launch_unprepare(Storage st, const uint8_t* in, size_t n, int dim, si
 }
 
 __global__ void set_flags_kernel(uint8_t* flags, const uint32_t* slots, size_t n, uint8_t value) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flags[slots[i]] = value;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        flags[slots[i]] = value;
 }
 
 hipError_t launch_set_flags(uint8_t* flags, const uint32_t* slots, size_t n, uint8_t value, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(set_flags_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, flags, slots, n,
-                       value);
+    hipLaunchKernelGGL(set_flags_kernel, dim3(capped_grid(n, 256)), dim3(256), 0, s, flags, slots, n, value);
     return hipGetLastError();
 }
 
@@ -115,47 +127,48 @@ __device__ inline float normal_at(uint64_t base, uint64_t idx) {
 }
 
 __global__ void gen_normal_kernel(uint64_t base, size_t count, float scale, float* out) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < count) out[i] = normal_at(base, i) / scale;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = normal_at(base, i) / scale;
 }
 
+// kind 0 (clustered) / 3 (SIFT-like: ReLU, x48, rounded into 0..255); one wave per row
 __global__ __launch_bounds__(64) void gen_clustered_kernel(size_t n, int dim, uint64_t seed, size_t start,
                                                            const float* __restrict__ w,
-                                                           const float* __restrict__ centres,
+                                                           const float* __restrict__ centres, int sift,
                                                            float* __restrict__ out) {
     __shared__ float lat[LATENT];
-    const size_t r = blockIdx.x;
     const int lane = threadIdx.x;
-    const uint64_t row = start + r;
-    const uint64_t cl = splitmix64(splitmix64(seed ^ TAG_CLUSTER) + row) % N_CENTRES;
+    const uint64_t cbase = splitmix64(seed ^ TAG_CLUSTER);
     const uint64_t lbase = splitmix64(seed ^ TAG_LATENT);
-    lat[lane] = centres[cl * LATENT + lane] + 0.5f * normal_at(lbase, row * LATENT + lane);
-    __syncthreads();
     const uint64_t nbase = splitmix64(seed ^ TAG_NOISE);
-    for (int j = lane; j < dim; j += 64) {
-        float acc = 0.f;
-        for (int l = 0; l < LATENT; ++l) acc += lat[l] * w[(size_t)l * dim + j];
-        out[r * dim + j] = acc + 0.05f * normal_at(nbase, row * (uint64_t)dim + j);
+    for (size_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const uint64_t row = start + r;
+        const uint64_t cl = splitmix64(cbase + row) % N_CENTRES;
+        __syncthreads();  // previous row's readers are done with lat[]
+        lat[lane] = centres[cl * LATENT + lane] + 0.5f * normal_at(lbase, row * LATENT + lane);
+        __syncthreads();
+        for (int j = lane; j < dim; j += 64) {
+            float acc = 0.f;
+            for (int l = 0; l < LATENT; ++l) acc += lat[l] * w[(size_t)l * dim + j];
+            float v = acc + 0.05f * normal_at(nbase, row * (uint64_t)dim + j);
+            if (sift) v = fminf(255.f, rintf(fmaxf(v, 0.f) * 48.f));
+            out[r * dim + j] = v;
+        }
     }
 }
 
 __global__ void gen_gauss_kernel(size_t n, int dim, uint64_t seed, size_t start, float* out) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n * (size_t)dim) return;
+    const size_t tot = n * (size_t)dim;
     const uint64_t nbase = splitmix64(seed ^ TAG_NOISE);
-    out[i] = normal_at(nbase, start * (uint64_t)dim + i);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = normal_at(nbase, start * (uint64_t)dim + i);
 }
 
 __global__ void gen_u8_kernel(size_t n, int dim, uint64_t seed, size_t start, float* out) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n * (size_t)dim) return;
+    const size_t tot = n * (size_t)dim;
     const uint64_t b = splitmix64(seed ^ TAG_U8);
-    out[i] = (float)(splitmix64(b + start * (uint64_t)dim + i) % 256);
-}
-
-__global__ void sift_transform_kernel(size_t tot, float* out) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < tot) out[i] = fminf(255.f, rintf(fmaxf(out[i], 0.f) * 48.f));
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = (float)(splitmix64(b + start * (uint64_t)dim + i) % 256);
 }
 
 hipError_t launch_datagen(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed, size_t start_row,
@@ -164,19 +177,17 @@ hipError_t launch_datagen(int kind, size_t n, size_t dim, uint64_t seed, uint64_
     const size_t tot = n * dim;
     if (kind == 0 || kind == 3) {
         const size_t nw = (size_t)LATENT * dim, ncen = (size_t)N_CENTRES * LATENT;
-        hipLaunchKernelGGL(gen_normal_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s,
+        hipLaunchKernelGGL(gen_normal_kernel, dim3(capped_grid(nw, 256)), dim3(256), 0, s,
                            splitmix64(model_seed ^ TAG_PROJ), nw, 8.0f, scratch_w);
-        hipLaunchKernelGGL(gen_normal_kernel, dim3((unsigned)((ncen + 255) / 256)), dim3(256), 0, s,
+        hipLaunchKernelGGL(gen_normal_kernel, dim3(capped_grid(ncen, 256)), dim3(256), 0, s,
                            splitmix64(model_seed ^ TAG_CENTRE), ncen, 1.0f, scratch_c);
-        hipLaunchKernelGGL(gen_clustered_kernel, dim3((unsigned)n), dim3(64), 0, s, n, (int)dim, seed, start_row,
-                           scratch_w, scratch_c, out);
-        if (kind == 3)
-            hipLaunchKernelGGL(sift_transform_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, tot, out);
+        hipLaunchKernelGGL(gen_clustered_kernel, dim3(capped_grid(n, 1)), dim3(64), 0, s, n, (int)dim, seed,
+                           start_row, scratch_w, scratch_c, kind == 3 ? 1 : 0, out);
     } else if (kind == 1) {
-        hipLaunchKernelGGL(gen_gauss_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, n, (int)dim,
-                           seed, start_row, out);
+        hipLaunchKernelGGL(gen_gauss_kernel, dim3(capped_grid(tot, 256)), dim3(256), 0, s, n, (int)dim, seed,
+                           start_row, out);
     } else {
-        hipLaunchKernelGGL(gen_u8_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, n, (int)dim, seed,
+        hipLaunchKernelGGL(gen_u8_kernel, dim3(capped_grid(tot, 256)), dim3(256), 0, s, n, (int)dim, seed,
                            start_row, out);
     }
     return hipGetLastError();

@@ -17,11 +17,10 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
-#include <unordered_map>
-#include <unordered_set>
 #include <vector>
 
 #include "../../include/vsg.h"
+#include "keymap.hpp"
 #include "vsg_kernels.hpp"
 
 namespace vsg {
@@ -114,7 +113,7 @@ struct vsg_index {
     unsigned long long* d_stats = nullptr;  // [0..2] search, [3..4] build
 
     std::vector<int8_t> h_levels;
-    std::unordered_map<uint64_t, uint32_t> key2slot;
+    KeyMap keys;  // live key -> slot
     uint32_t entry = 0xFFFFFFFFu;
     int max_level = -1;
     std::atomic<uint64_t> build_vectors{0}, build_batches{0};
@@ -260,14 +259,25 @@ static int ensure_pairs(vsg_index* h, size_t n) {
     return VSG_OK;
 }
 
-// Validates keys (no reserved key, no live duplicate, none inside the batch).
-static int check_keys(vsg_index* h, const uint64_t* keys, size_t n) {
-    std::unordered_set<uint64_t> seen;
-    seen.reserve(n * 2);
+static void unmap_keys(vsg_index* h, const uint64_t* keys, size_t n) {
+    for (size_t i = 0; i < n; ++i) h->keys.erase(keys[i], nullptr);
+}
+
+// Maps keys[i] -> s0 + i.  Any reserved key, live duplicate or duplicate inside
+// the batch rejects the whole call (usearch: duplicate keys not allowed) and
+// leaves the map unchanged.
+static int map_keys(vsg_index* h, const uint64_t* keys, size_t n, uint32_t s0) {
+    h->keys.reserve(h->keys.size() + n);
     for (size_t i = 0; i < n; ++i) {
-        if (keys[i] == VSG_NO_KEY) return fail(VSG_EINVAL, "key UINT64_MAX is reserved");
-        if (h->key2slot.count(keys[i])) return fail(VSG_EDUPKEY, "Duplicate keys not allowed: " + std::to_string(keys[i]));
-        if (!seen.insert(keys[i]).second) return fail(VSG_EDUPKEY, "Duplicate key inside batch: " + std::to_string(keys[i]));
+        const uint64_t k = keys[i];
+        int code = VSG_OK;
+        if (k >= KeyMap::DEAD) code = VSG_EINVAL;
+        else if (!h->keys.insert(k, s0 + (uint32_t)i)) code = VSG_EDUPKEY;
+        if (code != VSG_OK) {
+            unmap_keys(h, keys, i);
+            return code == VSG_EINVAL ? fail(code, "keys UINT64_MAX and UINT64_MAX-1 are reserved")
+                                      : fail(code, "Duplicate keys not allowed: " + std::to_string(k));
+        }
     }
     return VSG_OK;
 }
@@ -290,7 +300,6 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
     HIP_TRY(hipMemcpyAsync(h->d_upper_off + s0, upper_off.data(), n * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_keys + s0, keys, n * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(h->d_flags + s0, 0, n, st));
-    for (size_t i = 0; i < n; ++i) h->key2slot[keys[i]] = s0 + (uint32_t)i;
     h->slots += n;
     h->live += n;
     if (h->opt.flags & VSG_FLAG_EXACT_ONLY) {  // vectors only: no graph
@@ -492,8 +501,11 @@ size_t vsg_index_dimensions(const vsg_index_t* h) { return h ? (size_t)h->dim : 
 int vsg_index_contains(const vsg_index_t* h, uint64_t key) {
     if (!h) return 0;
     std::shared_lock<std::shared_mutex> lk(h->mu);
-    return h->key2slot.count(key) ? 1 : 0;
+    return h->keys.find(key, nullptr) ? 1 : 0;
 }
+
+static int add_rows(vsg_index_t* h, const uint64_t* keys, const float* vecs, size_t n, bool device_src,
+                    hipStream_t user_stream, uint32_t s0);
 
 static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, size_t n, bool device_src,
                       hipStream_t user_stream) {
@@ -501,8 +513,7 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
     if (n == 0) return VSG_OK;
     std::unique_lock<std::shared_mutex> lk(h->mu);
     DeviceGuard dg(h->device);
-    int rc = check_keys(h, keys, n);
-    if (rc) return rc;
+    int rc;
     if (h->slots + n > MAX_SLOTS) return fail(VSG_EINVAL, "index full (2^29 slots per shard)");
     if (h->slots + n > h->cap) {
         size_t want = std::max<size_t>(h->cap * 2, 1024);
@@ -510,6 +521,16 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
         if ((rc = reserve_locked(h, std::min<size_t>(want, MAX_SLOTS)))) return rc;
     }
     const uint32_t s0 = (uint32_t)h->slots;
+    if ((rc = map_keys(h, keys, n, s0))) return rc;
+    rc = add_rows(h, keys, vecs, n, device_src, user_stream, s0);
+    if (rc) unmap_keys(h, keys, n);
+    return rc;
+}
+
+// rows -> HBM (prepare: convert / normalise / |x|^2), then the batched graph build
+static int add_rows(vsg_index_t* h, const uint64_t* keys, const float* vecs, size_t n, bool device_src,
+                    hipStream_t user_stream, uint32_t s0) {
+    int rc;
     if (device_src) {
         // order after the producer of `vecs` on the caller's stream (NULL = default stream)
         hipEvent_t ev;
@@ -552,10 +573,9 @@ int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_r
     DeviceGuard dg(h->device);
     std::vector<uint32_t> slots;
     for (size_t i = 0; i < n; ++i) {
-        auto it = h->key2slot.find(keys[i]);
-        if (it == h->key2slot.end()) continue;
-        slots.push_back(it->second);
-        h->key2slot.erase(it);
+        uint32_t slot;
+        if (!h->keys.erase(keys[i], &slot)) continue;
+        slots.push_back(slot);
     }
     if (!slots.empty()) {
         uint32_t* d = nullptr;
@@ -651,7 +671,8 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         HIP_TRY(launch_search(h->st, h->mk, p, s));
     } else {
         const size_t slots = h->slots;
-        int nblocks = (int)std::max<size_t>(1, (slots + 4095) / 4096);
+        // grid.y = row blocks (<= 65535 per dimension)
+        int nblocks = (int)std::min<size_t>(32768, std::max<size_t>(1, (slots + 4095) / 4096));
         const int rpb = (int)((slots + nblocks - 1) / nblocks);
         if (slots == 0) nblocks = 1;
         float* pd = nullptr;
@@ -872,7 +893,7 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
     h->live = 0;
     for (size_t i = 0; i < slots; ++i)
         if (!(removed[i] & 1)) {
-            h->key2slot[keys[i]] = (uint32_t)i;
+            h->keys.insert(keys[i], (uint32_t)i);
             h->live++;
         }
     h->entry = entry;

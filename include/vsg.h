@@ -76,9 +76,14 @@ typedef struct {
     uint64_t search_distances;   /* n_dist, summed over queries */
     uint64_t search_adjacency;   /* n_adj rows read */
     uint64_t build_vectors;
-    uint64_t build_distances;
+    uint64_t build_distances;    /* all build distance evaluations (sum of the next three + beam) */
     uint64_t build_adjacency;
     uint64_t build_batches;
+    uint64_t build_select_distances;   /* forward heuristic neighbour selection */
+    uint64_t reverse_recompute_distances; /* reverse links: distances to existing neighbours */
+    uint64_t reverse_select_distances; /* reverse links: heuristic re-selection */
+    uint64_t reverse_prunes;           /* (level, node) segments that overflowed and were re-selected */
+    uint64_t reverse_appends;          /* segments appended without re-selection */
 } vsg_stats_t;
 
 /* replaces usearch::Index::new(&options) — src/index/usearch.rs:98 */

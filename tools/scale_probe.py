@@ -40,7 +40,13 @@ def main():
     out = {"rows": rows, "dim": dim, "metric": metric, "quant": quant, "data": data, "batch_max": bmax,
            "build_s": round(bt, 2), "build_dist_per_vec": round(st["build_distances"] / rows, 1),
            "batches": st["build_batches"], "sample_rows_nonzero": float(np.mean(np.abs(xs).sum(1) > 0)),
-           "gt_valid": float(np.mean(gt >= 0)), "recall": {}}
+           "gt_valid": float(np.mean(gt >= 0)), "recall": {},
+           "build_breakdown_per_vec": {f: round(st[f] / rows, 2) for f in (
+               "build_select_distances", "reverse_recompute_distances", "reverse_select_distances",
+               "reverse_prunes", "reverse_appends", "build_adjacency")}}
+    out["build_breakdown_per_vec"]["beam_distances"] = round(
+        (st["build_distances"] - st["build_select_distances"] - st["reverse_recompute_distances"]
+         - st["reverse_select_distances"]) / rows, 1)
     info = idx.graph_info()
     out["max_level"] = info["max_level"]
     if ex is not None:

@@ -19,17 +19,24 @@
 
 namespace vsg {
 
-static __host__ __device__ inline int hash_size_for(int ef) {
-    int h = 1024;
-    while (h < 32 * ef && h < 16384) h <<= 1;
-    return h;
+// Visited-table entries: `factor` x ef (the traversal evaluates ~15-20 x ef
+// nodes), multiple of 64, within [1024, 16384].  Smaller tables raise the
+// number of co-resident waves per CU (LDS-bound occupancy at large ef) at the
+// cost of re-evaluating forgotten nodes; results do not depend on it.
+__host__ __device__ int hash_size_for(int ef, int factor) {
+    long h = (long)factor * ef;
+    h = (h + 63) & ~63L;
+    if (h < 1024) h = 1024;
+    if (h > 16384) h = 16384;
+    return (int)h;
 }
 
-size_t search_lds_bytes(int ef) {
-    return (size_t)hash_size_for(ef) * 4 + (size_t)ef * 16 + 64 * 4 * 4;
+static size_t wave_lds_bytes(int hash, int cap, bool with_sel) {
+    return (size_t)hash * 4 + (size_t)cap * 16 + 64 * 4 * 4 + (with_sel ? 64 * 4 * 2 : 0);
 }
 
-size_t insert_lds_bytes(int efc) { return search_lds_bytes(efc) + 64 * 4 * 2; }
+size_t search_lds_bytes(int ef, int hash) { return wave_lds_bytes(hash, ef, false); }
+size_t insert_lds_bytes(int efc, int hash) { return wave_lds_bytes(hash, efc, true); }
 
 static __device__ inline GraphDev to_dev(const DevGraph& g) {
     GraphDev d;
@@ -55,12 +62,11 @@ struct WaveLds {
     float* seld;
 };
 
-static __device__ inline WaveLds carve(uint8_t* smem, int cap, bool with_sel) {
+static __device__ inline WaveLds carve(uint8_t* smem, int cap, int hs, bool with_sel) {
     WaveLds w;
-    const int hs = hash_size_for(cap);
     uint8_t* p = smem;
     w.vis.tab = reinterpret_cast<uint32_t*>(p);
-    w.vis.mask = (uint32_t)hs - 1;
+    w.vis.size = (uint32_t)hs;
     p += (size_t)hs * 4;
     w.list.d0 = reinterpret_cast<float*>(p);
     p += (size_t)cap * 4;
@@ -237,7 +243,7 @@ __global__ __launch_bounds__(64) void hnsw_search_kernel(SearchParams p) {
     }
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
-    WaveLds w = carve(smem, p.ef, false);
+    WaveLds w = carve(smem, p.ef, p.hash_size, false);
     uint64_t ndist = 0, nadj = 0;
     int count = 0;
     uint64_t* ok = p.out_keys + (size_t)qi * p.k;
@@ -291,10 +297,11 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     const int bi = blockIdx.x;
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
-    WaveLds w = carve(smem, p.efc, true);
+    WaveLds w = carve(smem, p.efc, p.hash_size, true);
+    const uint64_t t_start = wall_clock64();
     const uint32_t node = p.nodes[bi];
     const int L = p.levels[bi];
-    uint64_t ndist = 0, nadj = 0;
+    uint64_t ndist = 0, nadj = 0, nsel_d = 0;
     QReg<G, VM, T> q;
     q.load(g.vec(node), g.nchunks);
     uint32_t cur = p.entry;
@@ -305,7 +312,7 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     for (int l = min(L, p.max_level); l >= 0; --l) {
         beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
         const int m = l == 0 ? g.M0 : g.M;
-        const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, m, ndist);
+        const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, m, nsel_d);
         uint32_t* row = g.row(node, l);
         if (lane < m) row[lane] = lane < nsel ? w.sel[lane] : VSG_EMPTY;
         if (lane < nsel) {
@@ -320,8 +327,12 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
         wave_sync();
     }
     if (lane == 0 && p.stats) {
-        atomicAdd(&p.stats[3], (unsigned long long)ndist);
+        atomicAdd(&p.stats[3], (unsigned long long)(ndist + nsel_d));
         atomicAdd(&p.stats[4], (unsigned long long)nadj);
+        atomicAdd(&p.stats[5], (unsigned long long)nsel_d);
+        const unsigned long long dt = wall_clock64() - t_start;
+        atomicAdd(&p.stats[10], dt);
+        atomicMax(&p.stats[11], dt);
     }
 }
 
@@ -336,11 +347,11 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
     const int cap = 2 * g.M0 > 64 ? 2 * g.M0 : 64;
-    WaveLds w = carve(smem, cap, true);
-    uint64_t ndist = 0, nadj = 0;
+    WaveLds w = carve(smem, cap, hash_size_for(cap, 32), true);
+    const uint64_t t_start = wall_clock64();
+    uint64_t ndist = 0, nadj = 0, nsel_d = 0, nprune = 0, nappend = 0;
     const size_t nw = gridDim.x;
-    size_t chunk = (p.npairs + nw - 1) / nw;
-    chunk = (chunk + 63) & ~(size_t)63;
+    const size_t chunk = (p.npairs + nw - 1) / nw;  // segments are found by their head pair
     const size_t beg = (size_t)blockIdx.x * chunk;
     const size_t end = min(beg + chunk, p.npairs);
     for (size_t i0 = beg; i0 < end; i0 += 64) {
@@ -378,8 +389,10 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
             const int ne = popc64(xm);
             if (ne + nin <= m) {
                 for (int t = lane; t < nin; t += 64) row[ne + t] = (uint32_t)(p.keys[h + t] & PAIR_ID_MASK);
+                ++nappend;
                 continue;
             }
+            ++nprune;
             QReg<G, VM, T> q;
             q.load(g.vec(v), g.nchunks);
             List& L = w.list;
@@ -404,14 +417,21 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
                 const uint32_t ci = valid ? (uint32_t)(p.keys[idx] & PAIR_ID_MASK) : 0u;
                 L.merge(valid, cd, ci, false, w.sd, w.si);
             }
-            const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, L.size, m, ndist);
+            const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, L.size, m, nsel_d);
             if (lane < m) row[lane] = lane < nsel ? w.sel[lane] : VSG_EMPTY;
             wave_sync();
         }
     }
     if (lane == 0 && p.stats) {
-        atomicAdd(&p.stats[3], (unsigned long long)ndist);
+        atomicAdd(&p.stats[3], (unsigned long long)(ndist + nsel_d));
         atomicAdd(&p.stats[4], (unsigned long long)nadj);
+        atomicAdd(&p.stats[6], (unsigned long long)ndist);
+        atomicAdd(&p.stats[7], (unsigned long long)nsel_d);
+        atomicAdd(&p.stats[8], (unsigned long long)nprune);
+        atomicAdd(&p.stats[9], (unsigned long long)nappend);
+        const unsigned long long dt = wall_clock64() - t_start;
+        atomicAdd(&p.stats[12], dt);
+        atomicMax(&p.stats[13], dt);
     }
 }
 
@@ -421,7 +441,7 @@ bool shape_supported(int nchunks) { return nchunks >= 1 && nchunks <= 1024; }
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s) {
     if (p.nq <= 0) return hipSuccess;
-    const size_t lds = search_lds_bytes(p.ef);
+    const size_t lds = search_lds_bytes(p.ef, p.hash_size);
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(hnsw_search_kernel, sh, tt, mt);
@@ -444,7 +464,7 @@ hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipSt
 
 hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s) {
     if (p.nnodes <= 0) return hipSuccess;
-    const size_t lds = insert_lds_bytes(p.efc);
+    const size_t lds = insert_lds_bytes(p.efc, p.hash_size);
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(hnsw_insert_kernel, sh, tt, mt);
@@ -458,7 +478,7 @@ hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipSt
 hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s) {
     if (p.npairs == 0) return hipSuccess;
     const int cap = 2 * p.g.M0 > 64 ? 2 * p.g.M0 : 64;
-    const size_t lds = insert_lds_bytes(cap);
+    const size_t lds = insert_lds_bytes(cap, hash_size_for(cap, 32));
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(hnsw_reverse_kernel, sh, tt, mt);

@@ -157,27 +157,30 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
 
 struct Visited {
     uint32_t* tab;
-    uint32_t mask;  // size - 1 (power of two)
+    uint32_t size;  // entries (multiple of 4, any value: slots via multiply-high)
 
     __device__ __forceinline__ void clear() {
         const int lane = lane_id();
         uint4* t4 = reinterpret_cast<uint4*>(tab);
-        const uint32_t n4 = (mask + 1) / 4;
+        const uint32_t n4 = size / 4;
         for (uint32_t i = lane; i < n4; i += 64) t4[i] = make_uint4(VSG_EMPTY, VSG_EMPTY, VSG_EMPTY, VSG_EMPTY);
         wave_sync();
     }
 
     // true if id was not present (inserted now, or the table could not record
-    // it: then `unrecorded` is set and the caller de-duplicates).
+    // it: then `unrecorded` is set and the caller de-duplicates).  A lost entry
+    // never changes the traversal, only adds a distance evaluation: a node seen
+    // before is either still in the top-ef list (de-duplicated there) or worse
+    // than the list's current worst entry (rejected by the merge threshold).
     __device__ __forceinline__ bool insert(uint32_t id, bool& unrecorded) {
-        uint32_t h = (id * 2654435761u) & mask;
+        uint32_t h = __umulhi(id * 2654435761u, size);
         unrecorded = false;
 #pragma unroll 1
         for (int p = 0; p < 32; ++p) {
             const uint32_t old = atomicCAS(&tab[h], VSG_EMPTY, id);
             if (old == VSG_EMPTY) return true;
             if (old == id) return false;
-            h = (h + 1) & mask;
+            h = h + 1 == size ? 0 : h + 1;
         }
         unrecorded = true;
         return true;

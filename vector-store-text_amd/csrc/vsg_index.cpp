@@ -132,7 +132,7 @@ struct vsg_index {
     size_t stage_cap = 0;  // rows
 
     mutable std::shared_mutex mu;
-    int reverse_grid = 2048;
+    int reverse_grid = 1 << 20;
 
     DevGraph graph() const {
         DevGraph g;
@@ -376,6 +376,7 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
         ip.entry = h->entry;
         ip.max_level = h->max_level;
         ip.efc = h->efc;
+        ip.hash_size = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", 32));
         ip.stats = h->d_stats;
         HIP_TRY(launch_insert(h->st, h->mk, ip, st));
 
@@ -396,7 +397,11 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
         rp.vals = h->d_pv[1];
         rp.npairs = npairs;
         rp.stats = h->d_stats;
-        const int grid = (int)std::max<size_t>(1, std::min<size_t>((size_t)h->reverse_grid, (npairs + 63) / 64));
+        // a few pairs per wave: the cost is in the few segments that need a
+        // heuristic re-selection, so spread them over as many waves as possible
+        const size_t rgrid = (size_t)env_double("VSG_REVERSE_GRID", (double)h->reverse_grid);
+        const size_t ppw = std::max<size_t>(1, (size_t)env_double("VSG_REVERSE_PAIRS_PER_WAVE", 16));
+        const int grid = (int)std::max<size_t>(1, std::min<size_t>(rgrid, (npairs + ppw - 1) / ppw));
         HIP_TRY(launch_reverse(h->st, h->mk, rp, grid, st));
 
         if (new_top >= 0) {
@@ -668,6 +673,7 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         p.out_counts = oc;
         p.stats = h->d_stats;
         p.xcd_map = env_double("VSG_SEARCH_XCD_MAP", 0) != 0 ? 1 : 0;
+        p.hash_size = hash_size_for(p.ef, (int)env_double("VSG_SEARCH_HASH_FACTOR", 32));
         HIP_TRY(launch_search(h->st, h->mk, p, s));
     } else {
         const size_t slots = h->slots;
@@ -812,6 +818,20 @@ int vsg_index_stats(const vsg_index_t* h, vsg_stats_t* out) {
     out->build_adjacency = s[4];
     out->build_vectors = h->build_vectors.load();
     out->build_batches = h->build_batches.load();
+    out->build_select_distances = s[5];
+    out->reverse_recompute_distances = s[6];
+    out->reverse_select_distances = s[7];
+    out->reverse_prunes = s[8];
+    out->reverse_appends = s[9];
+    return VSG_OK;
+}
+
+// Not part of the ABI (tools only): the raw kernel counter block.
+// [10]/[11] insert-wave wall-clock (100 MHz) sum / max, [12]/[13] reverse-wave.
+extern "C" int vsg_debug_counters(const vsg_index_t* h, uint64_t* out16) {
+    if (!h || !out16) return fail(VSG_EINVAL, "null argument");
+    DeviceGuard dg(h->device);
+    HIP_TRY(hipMemcpy(out16, h->d_stats, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return VSG_OK;
 }
 

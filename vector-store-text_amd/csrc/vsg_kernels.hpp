@@ -32,6 +32,7 @@ struct SearchParams {
     uint32_t* out_counts;
     unsigned long long* stats;  // [0] n_dist, [1] n_adj, [2] queries
     int xcd_map;                // 1: workgroups b, b+8, ... (one XCD) take consecutive queries
+    int hash_size;              // visited-table entries (hash_size_for)
 };
 
 struct InsertParams {
@@ -45,7 +46,8 @@ struct InsertParams {
     uint32_t entry;
     int max_level;
     int efc;
-    unsigned long long* stats;  // [3] n_dist, [4] n_adj
+    int hash_size;              // visited-table entries (hash_size_for)
+    unsigned long long* stats;  // [3] n_dist, [4] n_adj, [5] selection
 };
 
 struct ReverseParams {
@@ -107,8 +109,9 @@ constexpr uint64_t PAIR_ID_MASK = (1ull << 29) - 1;
 constexpr uint32_t MAX_SLOTS = 1u << 29;
 
 bool shape_supported(int nchunks);
-size_t search_lds_bytes(int ef);
-size_t insert_lds_bytes(int efc);
+__host__ __device__ int hash_size_for(int ef, int factor);
+size_t search_lds_bytes(int ef, int hash);
+size_t insert_lds_bytes(int efc, int hash);
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
 hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s);

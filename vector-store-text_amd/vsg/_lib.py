@@ -60,6 +60,11 @@ class Stats(C.Structure):
         ("build_distances", C.c_uint64),
         ("build_adjacency", C.c_uint64),
         ("build_batches", C.c_uint64),
+        ("build_select_distances", C.c_uint64),
+        ("reverse_recompute_distances", C.c_uint64),
+        ("reverse_select_distances", C.c_uint64),
+        ("reverse_prunes", C.c_uint64),
+        ("reverse_appends", C.c_uint64),
     ]
 
 

@@ -206,6 +206,34 @@ def test_hnsw_search_same_graph_bitexact(metric, dim, M):
         np.testing.assert_array_equal(m.distances, od)
 
 
+def test_hnsw_forgetful_visited_table_is_exact(monkeypatch):
+    """A visited table far smaller than the visited set (it forgets and the
+    top-ef list de-duplicates) must not change results: bit-exact vs the
+    oracle at ef = 400 over 6000 rows, and the same GPU-built graph whatever
+    the build table size."""
+    n, dim = 6000, 32
+    x = G.uint8_valued(n, dim, 41).astype(np.float32)
+    q = G.uint8_valued(64, dim, 42).astype(np.float32)
+    h = O.HnswOracle(dim, "l2sq", 8, 64, 48, seed=3)
+    h.add(np.arange(n), x)
+    idx = vsg.Index(dim, "l2sq", connectivity=8, expansion_add=64, expansion_search=48, seed=3)
+    idx.import_graph(h.export())
+    ok, od, oc = h.search(q, 20, 400)
+    for factor in ("1", "64"):
+        monkeypatch.setenv("VSG_SEARCH_HASH_FACTOR", factor)
+        m = idx.search(q, 20, 400)
+        np.testing.assert_array_equal(m.keys, ok)
+        np.testing.assert_array_equal(m.distances, od)
+    graphs = []
+    for factor in ("1", "32"):
+        monkeypatch.setenv("VSG_BUILD_HASH_FACTOR", factor)
+        b = vsg.Index(dim, "l2sq", connectivity=8, expansion_add=200, expansion_search=48, seed=3)
+        b.add(np.arange(n), x)
+        graphs.append(b.export())
+    np.testing.assert_array_equal(graphs[0]["adj0"], graphs[1]["adj0"])
+    np.testing.assert_array_equal(graphs[0]["upper"], graphs[1]["upper"])
+
+
 @pytest.mark.parametrize("metric,dim,quant", [("l2sq", 64, "f32"), ("cos", 128, "f32"),
                                               ("ip", 96, "f32"), ("l2sq", 64, "f16")])
 def test_hnsw_gpu_build_recall_vs_oracle(metric, dim, quant):

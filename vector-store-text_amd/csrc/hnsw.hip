@@ -22,7 +22,8 @@ namespace vsg {
 // Visited-table entries: `factor` x ef (the traversal evaluates ~15-20 x ef
 // nodes), multiple of 64, within [1024, 16384].  Smaller tables raise the
 // number of co-resident waves per CU (LDS-bound occupancy at large ef) at the
-// cost of re-evaluating forgotten nodes; results do not depend on it.
+// cost of re-evaluating forgotten nodes (Visited::insert); results do not
+// depend on it.
 __host__ __device__ int hash_size_for(int ef, int factor) {
     long h = (long)factor * ef;
     h = (h + 63) & ~63L;
@@ -154,6 +155,7 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
     List& L = w.list;
     L.cur = 0;
     L.size = 1;
+    bool lossy = false;  // the visited table has forgotten an id (wave-uniform)
     if (lane == 0) {
         bool unrec;
         w.vis.insert(ep, unrec);
@@ -170,10 +172,10 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
         const uint32_t* row = g.row(node, l);
         const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
         ++nadj;
-        bool fresh = false, unrec = false;
-        if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, unrec);
+        bool fresh = false, evicted = false;
+        if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
         const uint64_t mask = __ballot(fresh);
-        const bool any_unrec = __ballot(unrec) != 0;
+        lossy = lossy || __ballot(evicted) != 0;
         const int cnt = popc64(mask);
         if (fresh) w.todo[lanes_below(mask)] = nb;
         wave_sync();
@@ -185,7 +187,7 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
         const float cd = valid ? w.tdist[lane] : 0.f;
         const uint32_t ci = valid ? w.todo[lane] : 0u;
         wave_sync();
-        L.merge(valid, cd, ci, any_unrec, w.sd, w.si);
+        L.merge(valid, cd, ci, lossy, w.sd, w.si);
     }
 }
 

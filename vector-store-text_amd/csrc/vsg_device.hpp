@@ -167,22 +167,28 @@ struct Visited {
         wave_sync();
     }
 
-    // true if id was not present (inserted now, or the table could not record
-    // it: then `unrecorded` is set and the caller de-duplicates).  A lost entry
-    // never changes the traversal, only adds a distance evaluation: a node seen
-    // before is either still in the top-ef list (de-duplicated there) or worse
-    // than the list's current worst entry (rejected by the merge threshold).
-    __device__ __forceinline__ bool insert(uint32_t id, bool& unrecorded) {
-        uint32_t h = __umulhi(id * 2654435761u, size);
-        unrecorded = false;
+    // true if id was not present (it is recorded now).  A table that is too
+    // small forgets: after PROBES occupied slots the id overwrites its home slot
+    // and `evicted` is set; from then on the caller must treat every fresh id as
+    // possibly seen before and de-duplicate against the top-ef list.  Forgetting
+    // never changes the traversal, it only adds distance evaluations: a node seen
+    // before is either still in the list (de-duplicated there) or worse than the
+    // list's current worst entry (rejected by the merge threshold; entries only
+    // leave a full list).
+    template <int PROBES = 16>
+    __device__ __forceinline__ bool insert(uint32_t id, bool& evicted) {
+        const uint32_t h0 = __umulhi(id * 2654435761u, size);
+        uint32_t h = h0;
+        evicted = false;
 #pragma unroll 1
-        for (int p = 0; p < 32; ++p) {
+        for (int p = 0; p < PROBES; ++p) {
             const uint32_t old = atomicCAS(&tab[h], VSG_EMPTY, id);
             if (old == VSG_EMPTY) return true;
             if (old == id) return false;
             h = h + 1 == size ? 0 : h + 1;
         }
-        unrecorded = true;
+        atomicExch(&tab[h0], id);
+        evicted = true;
         return true;
     }
 };

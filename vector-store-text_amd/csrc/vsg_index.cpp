@@ -376,7 +376,7 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
         ip.entry = h->entry;
         ip.max_level = h->max_level;
         ip.efc = h->efc;
-        ip.hash_size = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", 32));
+        ip.hash_size = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", 16));
         ip.stats = h->d_stats;
         HIP_TRY(launch_insert(h->st, h->mk, ip, st));
 
@@ -673,7 +673,13 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         p.out_counts = oc;
         p.stats = h->d_stats;
         p.xcd_map = env_double("VSG_SEARCH_XCD_MAP", 0) != 0 ? 1 : 0;
-        p.hash_size = hash_size_for(p.ef, (int)env_double("VSG_SEARCH_HASH_FACTOR", 32));
+        {
+            // visited table: LDS is the occupancy limit at large ef, and a
+            // forgotten node costs one more row read -- cheap for short rows
+            const bool wide = h->row_bytes >= 1024;
+            const int factor = (int)env_double("VSG_SEARCH_HASH_FACTOR", wide ? 12 : 6);
+            p.hash_size = std::max(hash_size_for(p.ef, factor), wide ? 2048 : 1024);
+        }
         HIP_TRY(launch_search(h->st, h->mk, p, s));
     } else {
         const size_t slots = h->slots;

@@ -166,6 +166,56 @@ int vsg_index_import(vsg_index_t* index, size_t slots, const float* vectors,
 int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed,
                        size_t start_row, float* out_device, void* stream);
 
+/* ------------------------------------------------------------------ Actor --
+ * The reference's per-index actor (src/index/usearch.rs:82-311: an mpsc
+ * channel of Index::{AddOrReplace, Remove, Ann, Count} messages served by
+ * tokio/rayon tasks) with the GPU index behind it.  One worker thread per actor
+ * drains the message FIFO and turns runs of single-vector adds and single-query
+ * anns into batched GPU calls; capacity grows like
+ * usearch.rs:200-212.  Messages apply in submission order (an ann sees every
+ * write submitted before it).  Every function is thread-safe; errors are
+ * reported through vsg_last_error() like the index calls.  The PK<->u64
+ * bimap stays in the caller, as in the reference (usearch.rs:109-113). */
+typedef struct vsg_actor vsg_actor_t;
+
+typedef struct {
+    vsg_index_options_t index;
+    uint64_t reserve_increment; /* RESERVE_INCREMENT (usearch.rs:63); 0 => 1,000,000 */
+    uint64_t reserve_threshold; /* RESERVE_THRESHOLD (:67); 0 => increment / 3 */
+    uint32_t max_batch;         /* messages drained per worker wake-up; 0 => 65536 */
+    uint32_t max_wait_us;       /* optional coalescing window; 0 => natural batching */
+} vsg_actor_options_t;
+
+typedef struct {
+    uint64_t messages, writes, anns, counts;
+    uint64_t add_calls, remove_calls, search_calls, reserve_calls;
+    uint64_t add_errors, remove_errors, search_errors;
+    uint64_t max_search_batch, max_add_batch;
+} vsg_actor_counters_t;
+
+/* replaces usearch::new (the actor spawn + Index::new + reserve(1M)) — usearch.rs:82-139 */
+int vsg_actor_new(const vsg_actor_options_t* options, vsg_actor_t** out);
+/* drains queued messages, stops the worker, frees the index (channel close, :129) */
+void vsg_actor_free(vsg_actor_t* actor);
+/* Index::AddOrReplace — usearch.rs:174-233.  Asynchronous (the reference's
+ * channel send); failures inside the worker are counted (add_errors), as the
+ * reference logs and swallows them (:207-224). */
+int vsg_actor_add_or_replace(vsg_actor_t* actor, uint64_t key, const float* embedding, size_t dims);
+/* Index::Remove — usearch.rs:235-249 (asynchronous; unknown keys are ignored) */
+int vsg_actor_remove(vsg_actor_t* actor, uint64_t key);
+/* Index::Ann — usearch.rs:251-306.  Blocks until answered.  Dimension errors
+ * as :259-272.  out_*: `limit` entries, ascending, padded with VSG_NO_KEY/+inf
+ * past *out_count. */
+int vsg_actor_ann(vsg_actor_t* actor, const float* embedding, size_t dims, size_t limit,
+                  uint64_t* out_keys, float* out_distances, size_t* out_count);
+/* Index::Count — usearch.rs:308-311 (live size) */
+int vsg_actor_count(vsg_actor_t* actor, size_t* out);
+/* wait until all previously submitted messages are applied */
+int vsg_actor_flush(vsg_actor_t* actor);
+int vsg_actor_counters(const vsg_actor_t* actor, vsg_actor_counters_t* out);
+/* borrowed handle of the actor's index (stats, export); valid until vsg_actor_free */
+vsg_index_t* vsg_actor_index(vsg_actor_t* actor);
+
 /* splitmix64 level draw; bit-identical to oracle/vsg_oracle.c */
 int vsg_sample_level(uint64_t seed, uint64_t slot, uint32_t connectivity);
 

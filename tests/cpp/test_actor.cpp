@@ -1,0 +1,257 @@
+// Host logic of the coalescing index actor (csrc/actor.hpp) against a mock
+// backend: FIFO semantics of add/replace/remove, batching of concurrent anns,
+// ef grouping, capacity growth (src/index/usearch.rs:200-212), error counting.
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <map>
+#include <random>
+#include <thread>
+
+#include "../../vector-store-text_amd/csrc/actor.hpp"
+
+#define CHECK(c)                                                      \
+    do {                                                              \
+        if (!(c)) {                                                   \
+            std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c); \
+            std::exit(1);                                             \
+        }                                                             \
+    } while (0)
+
+struct Call {
+    char op;
+    size_t n, k, ef;
+};
+
+// exact l2sq over a std::map, ties by key; records every call
+struct Mock final : vsg::ActorBackend {
+    size_t dim, ef0, cap = 0;
+    std::map<uint64_t, std::vector<float>> rows;
+    std::vector<Call>* log;
+    std::vector<size_t>* reserves;
+    int search_sleep_us;
+    bool fail_add = false;
+    Mock(size_t d, size_t ef, std::vector<Call>* l, std::vector<size_t>* r, int sleep_us)
+        : dim(d), ef0(ef), log(l), reserves(r), search_sleep_us(sleep_us) {}
+    size_t dimensions() const override { return dim; }
+    size_t size() const override { return rows.size(); }
+    size_t capacity() const override { return cap; }
+    size_t expansion_search() const override { return ef0; }
+    bool contains(uint64_t k) const override { return rows.count(k) != 0; }
+    int reserve(size_t c) override {
+        reserves->push_back(c);
+        if (c > cap) cap = c;
+        return 0;
+    }
+    int add(const uint64_t* k, const float* v, size_t n) override {
+        log->push_back({'a', n, 0, 0});
+        if (fail_add) return 4;
+        for (size_t i = 0; i < n; ++i)
+            if (rows.count(k[i])) return 3;  // duplicate: nothing inserted
+        if (rows.size() + n > cap) return 2;
+        for (size_t i = 0; i < n; ++i) rows[k[i]] = std::vector<float>(v + i * dim, v + (i + 1) * dim);
+        return 0;
+    }
+    int remove(const uint64_t* k, size_t n, size_t* r) override {
+        log->push_back({'r', n, 0, 0});
+        size_t c = 0;
+        for (size_t i = 0; i < n; ++i) c += rows.erase(k[i]);
+        if (r) *r = c;
+        return 0;
+    }
+    int search(const float* q, size_t nq, size_t k, size_t ef, uint64_t* keys, float* dist,
+               size_t* counts) override {
+        log->push_back({'s', nq, k, ef});
+        if (search_sleep_us) std::this_thread::sleep_for(std::chrono::microseconds(search_sleep_us));
+        for (size_t i = 0; i < nq; ++i) {
+            std::vector<std::pair<float, uint64_t>> all;
+            for (auto& kv : rows) {
+                float s = 0;
+                for (size_t t = 0; t < dim; ++t) {
+                    const float df = kv.second[t] - q[i * dim + t];
+                    s += df * df;
+                }
+                all.push_back({s, kv.first});
+            }
+            std::sort(all.begin(), all.end());
+            const size_t c = std::min(k, all.size());
+            for (size_t j = 0; j < k; ++j) {
+                keys[i * k + j] = j < c ? all[j].second : ~0ull;
+                dist[i * k + j] = j < c ? all[j].first : INFINITY;
+            }
+            counts[i] = c;
+        }
+        return 0;
+    }
+};
+
+static std::vector<float> vec_of(uint64_t seed, size_t dim) {
+    std::mt19937_64 r(seed);
+    std::vector<float> v(dim);
+    for (auto& x : v) x = (float)(r() % 1000) / 10.f;
+    return v;
+}
+
+// 1) FIFO semantics: a random single-threaded add/replace/remove stream ends in
+//    the state a sequential map reaches, however the worker batches it.
+static void test_fifo_semantics() {
+    std::vector<Call> log;
+    std::vector<size_t> res;
+    auto* m = new Mock(4, 16, &log, &res, 0);
+    Mock* mp = m;
+    vsg::ActorConfig cfg;
+    cfg.reserve_increment = 64;
+    cfg.reserve_threshold = 21;
+    vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), cfg);
+    CHECK(a.init() == 0);
+    std::map<uint64_t, std::vector<float>> ref;
+    std::mt19937_64 rng(3);
+    for (int it = 0; it < 20000; ++it) {
+        const uint64_t k = rng() % 300;
+        if (rng() % 4 == 0) {
+            a.remove(k);
+            ref.erase(k);
+        } else {
+            auto v = vec_of(rng(), 4);
+            a.add_or_replace(k, v.data());
+            ref[k] = v;
+        }
+        if (it % 5000 == 4999) {
+            size_t n = 0;
+            CHECK(a.count(&n) == 0);
+            CHECK(n == ref.size());
+        }
+    }
+    CHECK(a.flush() == 0);
+    CHECK(mp->rows == ref);
+    const auto c = a.counters();
+    CHECK(c.add_errors == 0 && c.remove_errors == 0);
+    CHECK(c.writes == 20000);
+    CHECK(c.add_calls < 20000);  // coalesced
+    // capacity rule: every reserve adds one increment, only when free < threshold
+    for (size_t i = 1; i < res.size(); ++i) CHECK(res[i] == res[i - 1] + 64);
+    CHECK(mp->cap - mp->rows.size() >= 21 - 1);
+}
+
+// 2) concurrent anns are batched, and each answer equals the backend's own
+//    answer for that query alone.
+static void test_concurrent_anns() {
+    std::vector<Call> log;
+    std::vector<size_t> res;
+    auto* m = new Mock(8, 16, &log, &res, 2000);
+    vsg::ActorConfig cfg;
+    vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), cfg);
+    CHECK(a.init() == 0);
+    for (uint64_t k = 0; k < 500; ++k) {
+        auto v = vec_of(k + 100, 8);
+        a.add_or_replace(k, v.data());
+    }
+    CHECK(a.flush() == 0);
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    const int T = 32, Q = 40;
+    for (int t = 0; t < T; ++t) {
+        th.emplace_back([&, t] {
+            for (int i = 0; i < Q; ++i) {
+                auto q = vec_of(7000 + t * 1000 + i, 8);
+                const size_t k = 1 + (size_t)((t + i) % 12);
+                std::vector<uint64_t> keys(k);
+                std::vector<float> dist(k);
+                size_t cnt = 0;
+                if (a.ann(q.data(), 8, k, keys.data(), dist.data(), &cnt) != 0) { bad++; continue; }
+                // direct answer (mock is exact => top-k is a prefix of top-kmax)
+                std::vector<std::pair<float, uint64_t>> all;
+                for (uint64_t r = 0; r < 500; ++r) {
+                    auto v = vec_of(r + 100, 8);
+                    float s = 0;
+                    for (int d = 0; d < 8; ++d) s += (v[d] - q[d]) * (v[d] - q[d]);
+                    all.push_back({s, r});
+                }
+                std::sort(all.begin(), all.end());
+                if (cnt != k) bad++;
+                for (size_t j = 0; j < k; ++j)
+                    if (keys[j] != all[j].second || dist[j] != all[j].first) bad++;
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    CHECK(bad == 0);
+    const auto c = a.counters();
+    CHECK(c.anns == (uint64_t)(T * Q));
+    CHECK(c.search_calls < c.anns);  // batched
+    CHECK(c.max_search_batch > 1);
+}
+
+// 3) effective-ef grouping: one drained run with k below and above ef0 makes
+//    two searches, each at ef = max(ef0, k); wrong dims are rejected up front.
+static void test_ef_groups_and_errors() {
+    std::vector<Call> log;
+    std::vector<size_t> res;
+    auto* m = new Mock(2, 4, &log, &res, 20000);
+    vsg::ActorConfig cfg;
+    vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), cfg);
+    CHECK(a.init() == 0);
+    for (uint64_t k = 0; k < 50; ++k) {
+        float v[2] = {(float)k, 0.f};
+        a.add_or_replace(k, v);
+    }
+    CHECK(a.flush() == 0);
+    // occupy the worker with one slow search, queue a mixed run behind it
+    std::vector<std::thread> th;
+    std::atomic<int> bad{0};
+    for (int t = 0; t < 7; ++t) {
+        th.emplace_back([&, t] {
+            if (t) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+            float q[2] = {(float)t, 0.f};
+            const size_t k = t % 2 ? 2 : 9;  // ef = 4 or 9
+            std::vector<uint64_t> keys(k);
+            std::vector<float> dist(k);
+            size_t cnt = 0;
+            if (a.ann(q, 2, k, keys.data(), dist.data(), &cnt) != 0 || cnt != k || keys[0] != (uint64_t)t) bad++;
+        });
+    }
+    for (auto& x : th) x.join();
+    CHECK(bad == 0);
+    bool saw4 = false, saw9 = false;
+    for (auto& c : log)
+        if (c.op == 's') {
+            CHECK(c.ef == std::max<size_t>(4, c.k));
+            saw4 |= c.ef == 4;
+            saw9 |= c.ef == 9;
+        }
+    CHECK(saw4 && saw9);
+    float q[3] = {0, 0, 0};
+    uint64_t kk[1];
+    float dd[1];
+    CHECK(a.ann(q, 3, 1, kk, dd, nullptr) == 1);
+    CHECK(a.ann(q, 2, 0, kk, dd, nullptr) == 1);
+}
+
+// 4) add failures are counted and swallowed, later messages still apply
+static void test_add_errors_swallowed() {
+    std::vector<Call> log;
+    std::vector<size_t> res;
+    auto* m = new Mock(2, 4, &log, &res, 0);
+    Mock* mp = m;
+    vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), vsg::ActorConfig{});
+    CHECK(a.init() == 0);
+    mp->fail_add = true;
+    float v[2] = {1, 2};
+    a.add_or_replace(1, v);
+    CHECK(a.flush() == 0);
+    mp->fail_add = false;
+    a.add_or_replace(2, v);
+    size_t n = 0;
+    CHECK(a.count(&n) == 0 && n == 1);
+    CHECK(a.counters().add_errors == 1);
+}
+
+int main() {
+    test_fifo_semantics();
+    test_concurrent_anns();
+    test_ef_groups_and_errors();
+    test_add_errors_swallowed();
+    std::printf("ok\n");
+    return 0;
+}

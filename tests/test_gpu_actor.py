@@ -1,0 +1,163 @@
+"""GPU: the coalescing actor (include/vsg.h "Actor") behind the reference's
+message API (src/index/usearch.rs:141-311)."""
+import ctypes as C
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+import vsg
+from vsg import datagen as G
+from vsg._lib import check, lib
+from vsg.actor import Actor, UsearchIndex, new_usearch
+
+from test_gpu_parity import _kats
+
+pytestmark = pytest.mark.gpu
+
+
+def _direct_search(actor, q, k, ef):
+    h = lib().vsg_actor_index(actor._h)
+    nq = q.shape[0]
+    keys = np.empty((nq, k), np.uint64)
+    dist = np.empty((nq, k), np.float32)
+    cnt = np.empty(nq, np.uint64)
+    q = np.ascontiguousarray(q, np.float32)
+    check(lib().vsg_index_search(h, C.c_void_p(q.ctypes.data), nq, k, ef, C.c_void_p(keys.ctypes.data),
+                                 C.c_void_p(dist.ctypes.data), C.c_void_p(cnt.ctypes.data)))
+    return keys, dist, cnt
+
+
+@pytest.mark.parametrize("metric", ["l2sq", "ip"])
+def test_actor_reference_unit_kat(metric):
+    """src/index/usearch.rs:322-425 through the factory / IndexExt surface."""
+    kat = _kats()["unit_actor"]
+    idx = new_usearch(metric=metric).create_index("ks.idx", kat["dimensions"])
+    for st in kat["steps"]:
+        if st["op"] == "add_or_replace":
+            idx.add_or_replace(tuple(st["pk"]), st["embedding"])
+        elif st["op"] == "remove":
+            idx.remove(tuple(st["pk"]))
+        elif st["op"] == "count":
+            assert idx.count() == st["expect"]
+        else:
+            pks, dists = idx.ann(st["embedding"], st["limit"])
+            assert len(pks) == 1 and len(dists) == 1
+            assert list(pks[0]) == st["expect_pk"]
+    idx.close()
+
+
+@pytest.mark.parametrize("metric", ["l2sq", "ip"])
+def test_actor_reference_integration_kat(metric):
+    """tests/integration/usearch.rs:74-123."""
+    kat = _kats()["integration"]
+    idx = new_usearch(metric=metric).create_index("ks.idx", kat["dimensions"])
+    for pk, emb in kat["rows"]:
+        idx.add_or_replace(tuple(pk), emb)
+    assert idx.count() == kat["count"]
+    pks, _ = idx.ann(kat["ann"]["embedding"], kat["ann"]["limit"])
+    assert list(pks[0]) == kat["ann"]["expect_pk"]
+    idx.close()
+
+
+def test_actor_errors_match_reference():
+    idx = UsearchIndex(4)
+    with pytest.raises(vsg.VsgError, match="ann: embedding dimensions == 0"):
+        idx.ann([], 1)
+    with pytest.raises(vsg.VsgError, match=r"ann: wrong embedding dimensions: 3 != 4"):
+        idx.ann([1, 2, 3], 1)
+    with pytest.raises(vsg.VsgError, match="wrong embedding dimensions"):
+        idx.actor.add_or_replace(1, [1, 2, 3])
+    assert idx.ann([0, 0, 0, 1], 5) == ([], [])  # empty index
+    idx.close()
+
+
+def test_actor_concurrent_anns_batched_and_exact():
+    """32 threads of single-query anns: answers equal the index's own batched
+    search of the same queries (batching changes nothing) and the worker
+    coalesced them."""
+    n, dim = 20000, 64
+    bs, qs, ms = G.config_seeds(1)
+    x = G.clustered(n, dim, bs, ms)
+    q = G.clustered(640, dim, qs, ms)
+    a = Actor(dim, "cos", connectivity=16, expansion_add=128, expansion_search=32, seed=4)
+    for i in range(n):
+        a.add_or_replace(i, x[i])
+    a.flush()
+    assert a.count() == n
+    c0 = a.counters()
+    assert c0["add_calls"] < n / 16, c0  # single-vector messages became batches
+    ks = [1 + (i % 3) * 7 for i in range(len(q))]  # k in {1, 8, 15}: ef = 32 for all
+    out = [None] * len(q)
+
+    def worker(t):
+        for i in range(t, len(q), 32):
+            out[i] = a.ann(q[i], ks[i])
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(32)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    c = a.counters()
+    assert c["anns"] == len(q)
+    assert c["search_calls"] < len(q) and c["max_search_batch"] > 1, c
+    dk, dd, dc = _direct_search(a, q, 15, 32)
+    for i in range(len(q)):
+        k, d = out[i]
+        assert len(k) == ks[i]
+        np.testing.assert_array_equal(k, dk[i, :ks[i]])
+        np.testing.assert_array_equal(d, dd[i, :ks[i]])
+    a.close()
+
+
+def test_actor_replace_remove_semantics_vs_oracle():
+    """A CDC-style upsert stream (replace = remove + add, removes of unknown
+    keys ignored) through the actor ends in the same live set as a dict; exact
+    answers over it equal the oracle's."""
+    dim = 16
+    rng = np.random.default_rng(5)
+    idx = UsearchIndex(dim, metric="l2sq")
+    live = {}
+    for it in range(6000):
+        pk = ("pk", int(rng.integers(0, 800)))
+        if rng.random() < 0.25:
+            idx.remove(pk)
+            live.pop(pk, None)
+        else:
+            v = rng.integers(0, 16, dim).astype(np.float32)
+            idx.add_or_replace(pk, v)
+            live[pk] = v
+    assert idx.count() == len(live)
+    # exact search on the actor's index == oracle over the live dict
+    h = lib().vsg_actor_index(idx.actor._h)
+    q = rng.integers(0, 16, (50, dim)).astype(np.float32)
+    keys = np.empty((50, 10), np.uint64)
+    dist = np.empty((50, 10), np.float32)
+    check(lib().vsg_index_exact_search(h, C.c_void_p(q.ctypes.data), 50, 10, C.c_void_p(keys.ctypes.data),
+                                       C.c_void_p(dist.ctypes.data), None))
+    pks = list(live)
+    mat = np.stack([live[p] for p in pks])
+    # oracle ties break by row order; compare distances exactly and the key
+    # sets up to ties
+    _, od, _ = O.exact_search("l2sq", mat, q, 10)
+    np.testing.assert_array_equal(dist, od)
+    for r in range(50):
+        got = {idx._key2pk[int(k)] for k in keys[r]}
+        for pk in got:
+            assert pk in live
+    idx.close()
+
+
+def test_actor_capacity_growth_rule():
+    """reserve(capacity + increment) whenever free < threshold (usearch.rs:200-212)."""
+    a = Actor(8, reserve_increment=1000, reserve_threshold=333)
+    assert a.capacity() == 1000
+    x = np.random.default_rng(1).standard_normal((5000, 8)).astype(np.float32)
+    for i in range(5000):
+        a.add_or_replace(i, x[i])
+    a.flush()
+    assert a.count() == 5000
+    cap = a.capacity()
+    assert cap % 1000 == 0 and cap - 5000 >= 333 - 1
+    assert a.counters()["reserve_calls"] >= 4
+    a.close()

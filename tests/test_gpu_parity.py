@@ -409,3 +409,28 @@ def test_export_import_gpu_roundtrip():
     ok, od, _ = h.search(q, 10, 32)
     np.testing.assert_array_equal(ma.keys, ok)
     np.testing.assert_array_equal(ma.distances, od)
+
+
+@pytest.mark.parametrize("dim,metric", [(128, "l2sq"), (768, "cos")])
+def test_search_batch_invariance(dim, metric):
+    """A query's answer does not depend on the batch it is searched in (the
+    actor's coalescing relies on it): one call of 20,000 queries == calls of
+    1 / 7 / 64 / 1000 queries, host-buffer and device API."""
+    import torch
+    n = 60000
+    bs, qs, ms = G.config_seeds(2)
+    x = vsg.datagen_device("clustered", n, dim, bs, ms)
+    q = vsg.datagen_device("clustered", 20000, dim, qs, ms)
+    idx = vsg.Index(dim, metric, "f32", 16, 128, 36, seed=1)
+    idx.add_device(np.arange(n, dtype=np.uint64), x)
+    qh = q.cpu().numpy()
+    full = idx.search(qh, 10, 36)
+    fk, fd = idx.search_device(q, 10, 36)
+    np.testing.assert_array_equal(fk.cpu().numpy().astype(np.uint64), full.keys)
+    np.testing.assert_array_equal(fd.cpu().numpy(), full.distances)
+    for bsz in (1, 7, 64, 1000):
+        for s in range(0, 2000 if bsz < 64 else 40000, bsz):
+            m = idx.search(qh[s:s + bsz], 10, 36)
+            np.testing.assert_array_equal(m.keys, full.keys[s:s + bsz], err_msg=f"batch {bsz} at {s}")
+            np.testing.assert_array_equal(m.distances, full.distances[s:s + bsz])
+    torch.cuda.synchronize()

@@ -1,0 +1,159 @@
+// actor_load — serving-path load generator for the coalescing actor
+// (include/vsg.h "Actor").  C clients (std::thread) issue blocking
+// single-query vsg_actor_ann calls, like the reference's per-request
+// Index::Ann messages (src/index/usearch.rs:251-306); reports QPS, latency
+// percentiles, how the worker batched them, and the same queries as one
+// batched vsg_index_search for comparison.
+//
+// build: make -C tools actor_load   (links ../vector-store-text_amd/lib/libvsg.so)
+// usage: actor_load rows dim metric(0 l2sq,1 ip,2 cos) clients queries_per_client k ef [max_wait_us]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "../include/vsg.h"
+
+#define TRY(x)                                                                    \
+    do {                                                                          \
+        int rc__ = (x);                                                           \
+        if (rc__) {                                                               \
+            std::fprintf(stderr, "%s failed: %d %s\n", #x, rc__, vsg_last_error()); \
+            return 1;                                                             \
+        }                                                                         \
+    } while (0)
+
+using clk = std::chrono::steady_clock;
+
+int main(int argc, char** argv) {
+    if (argc < 8) {
+        std::fprintf(stderr, "usage: %s rows dim metric clients qpc k ef [max_wait_us]\n", argv[0]);
+        return 2;
+    }
+    const size_t rows = std::strtoull(argv[1], nullptr, 10), dim = std::strtoull(argv[2], nullptr, 10);
+    const unsigned metric = (unsigned)std::atoi(argv[3]);
+    const int clients = std::atoi(argv[4]), qpc = std::atoi(argv[5]);
+    const size_t k = std::strtoull(argv[6], nullptr, 10), ef = std::strtoull(argv[7], nullptr, 10);
+    const unsigned wait_us = argc > 8 ? (unsigned)std::atoi(argv[8]) : 0;
+    const uint64_t cfg = 2, base_seed = 0x5EED0000 + cfg, q_seed = 0x5EED1000 + cfg, m_seed = 0x5EED2000 + cfg;
+
+    vsg_actor_options_t o{};
+    o.index.dimensions = (uint32_t)dim;
+    o.index.metric = metric;
+    o.index.connectivity = 16;
+    o.index.expansion_add = 128;
+    o.index.expansion_search = (uint32_t)ef;
+    o.index.seed = 1;
+    o.max_wait_us = wait_us;
+    vsg_actor_t* a = nullptr;
+    TRY(vsg_actor_new(&o, &a));
+    vsg_index_t* h = vsg_actor_index(a);
+
+    // base rows straight into the actor's index (setup, not the measured path)
+    float* d_x = nullptr;
+    if (hipMalloc(&d_x, rows * dim * 4) != hipSuccess) return 1;
+    TRY(vsg_datagen_device(0, rows, dim, base_seed, m_seed, 0, d_x, nullptr));
+    std::vector<uint64_t> keys(rows);
+    for (size_t i = 0; i < rows; ++i) keys[i] = i;
+    TRY(vsg_index_add_device(h, keys.data(), d_x, rows, nullptr));
+    (void)hipDeviceSynchronize();
+    (void)hipFree(d_x);
+
+    const size_t nq = (size_t)clients * qpc;
+    float* d_q = nullptr;
+    if (hipMalloc(&d_q, nq * dim * 4) != hipSuccess) return 1;
+    TRY(vsg_datagen_device(0, nq, dim, q_seed, m_seed, 0, d_q, nullptr));
+    std::vector<float> q(nq * dim);
+    (void)hipMemcpy(q.data(), d_q, nq * dim * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_q);
+
+    // batched reference: all queries in one call
+    std::vector<uint64_t> bk(nq * k);
+    std::vector<float> bd(nq * k);
+    std::vector<size_t> bc(nq);
+    TRY(vsg_index_search(h, q.data(), nq, k, ef, bk.data(), bd.data(), bc.data()));  // warm
+    std::vector<uint64_t> bk1 = bk;
+    auto t0 = clk::now();
+    TRY(vsg_index_search(h, q.data(), nq, k, ef, bk.data(), bd.data(), bc.data()));
+    const double batched_s = std::chrono::duration<double>(clk::now() - t0).count();
+
+    vsg_actor_counters_t c0{};
+    vsg_actor_counters(a, &c0);
+    std::vector<double> lat(nq);
+    std::vector<uint64_t> ak(nq * k);
+    std::atomic<int> mismatch{0}, errors{0};
+    auto client = [&](int t) {
+        std::vector<uint64_t> ok(k);
+        std::vector<float> od(k);
+        for (int i = 0; i < qpc; ++i) {
+            const size_t qi = (size_t)i * clients + t;
+            size_t cnt = 0;
+            auto s = clk::now();
+            if (vsg_actor_ann(a, &q[qi * dim], dim, k, ok.data(), od.data(), &cnt)) {
+                errors++;
+                continue;
+            }
+            lat[qi] = std::chrono::duration<double, std::micro>(clk::now() - s).count();
+            std::copy(ok.begin(), ok.end(), ak.begin() + qi * k);
+            for (size_t j = 0; j < k; ++j)
+                if (ok[j] != bk[qi * k + j] || od[j] != bd[qi * k + j]) {
+                    if (mismatch++ < 3)
+                        std::fprintf(stderr, "mismatch q%zu j%zu cnt %zu: %llu %.9g vs batched %llu %.9g\n", qi, j,
+                                     cnt, (unsigned long long)ok[j], od[j], (unsigned long long)bk[qi * k + j],
+                                     bd[qi * k + j]);
+                    break;
+                }
+        }
+    };
+    std::vector<std::thread> th;
+    t0 = clk::now();
+    for (int t = 0; t < clients; ++t) th.emplace_back(client, t);
+    for (auto& x : th) x.join();
+    const double served_s = std::chrono::duration<double>(clk::now() - t0).count();
+    vsg_actor_counters_t c1{};
+    vsg_actor_counters(a, &c1);
+    // diagnostics: does the batched answer itself drift after the load?
+    {
+        std::vector<uint64_t> bk2(nq * k);
+        std::vector<float> bd2(nq * k);
+        TRY(vsg_index_search(h, q.data(), nq, k, ef, bk2.data(), bd2.data(), bc.data()));
+        size_t d1 = 0, d2 = 0, first = nq;
+        for (size_t i = 0; i < nq; ++i) {
+            bool x = false, y = false;
+            for (size_t j = 0; j < k; ++j) {
+                x |= bk2[i * k + j] != bk[i * k + j];
+                y |= bk2[i * k + j] != ak[i * k + j];
+            }
+            d1 += x;
+            d2 += y;
+            if (x && first == nq) first = i;
+        }
+        size_t d0 = 0, f0 = nq;
+        for (size_t i = 0; i < nq; ++i)
+            for (size_t j = 0; j < k; ++j)
+                if (bk2[i * k + j] != bk1[i * k + j]) {
+                    d0++;
+                    if (f0 == nq) f0 = i;
+                    break;
+                }
+        std::fprintf(stderr, "batched-before vs batched-after: %zu rows differ (first %zu); warm call: %zu (first %zu); actor vs after: %zu\n", d1,
+                     first, d0, f0, d2);
+    }
+    std::sort(lat.begin(), lat.end());
+    const uint64_t calls = c1.search_calls - c0.search_calls;
+    std::printf(
+        "{\"rows\": %zu, \"dim\": %zu, \"clients\": %d, \"queries\": %zu, \"k\": %zu, \"ef\": %zu, "
+        "\"max_wait_us\": %u, \"actor_qps\": %.1f, \"batched_qps\": %.1f, \"lat_us_p50\": %.1f, "
+        "\"lat_us_p99\": %.1f, \"search_calls\": %llu, \"mean_batch\": %.1f, \"max_batch\": %llu, "
+        "\"mismatch_vs_batched\": %d, \"errors\": %d}\n",
+        rows, dim, clients, nq, k, ef, wait_us, nq / served_s, nq / batched_s, lat[nq / 2], lat[nq * 99 / 100],
+        (unsigned long long)calls, calls ? (double)nq / calls : 0.0, (unsigned long long)c1.max_search_batch,
+        mismatch.load(), errors.load());
+    vsg_actor_free(a);
+    return mismatch || errors ? 1 : 0;
+}

@@ -1,0 +1,382 @@
+// actor.hpp — the index actor of src/index/usearch.rs restated for a GPU
+// backend: one worker thread per index drains a FIFO of messages and turns
+// runs of single-vector / single-query messages into batched GPU calls
+// (SURVEY §8f row 1).  Header-only and HIP-free so the host logic is tested
+// with g++ against a mock backend (tests/cpp/test_actor.cpp).
+//
+// Reference behaviour mirrored (src/index/usearch.rs):
+//   * Index::{AddOrReplace, Remove, Ann, Count} messages          :141-172
+//   * capacity growth: free < RESERVE_THRESHOLD => reserve(capacity +
+//     RESERVE_INCREMENT), 1M / 333,333 by default                 :61-66, :200-212
+//   * replace = remove the live key, then add                      :214-221
+//   * add/remove failures are swallowed (counted here, logged there) :207-224, :246
+//   * ann dimension checks before any search                       :259-272
+//   * count = live size                                            :308-311
+// Ordering is stronger than the reference's (which spawns every message as
+// its own task): messages are applied in submission order, so an Ann sees every
+// write submitted before it.  Batching never changes a result: an Ann run is
+// split by effective ef = max(ef, k) and a query's top-k is the prefix of its
+// group's top-kmax (the search returns the first k live entries of its list).
+#pragma once
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace vsg {
+
+// What the actor needs from an index shard (implemented over vsg_index_t in
+// vsg_actor.cpp, and by a mock in the tests).  Return codes follow vsg.h.
+struct ActorBackend {
+    virtual ~ActorBackend() = default;
+    virtual size_t dimensions() const = 0;
+    virtual size_t size() const = 0;
+    virtual size_t capacity() const = 0;
+    virtual size_t expansion_search() const = 0;
+    virtual bool contains(uint64_t key) const = 0;
+    virtual int reserve(size_t capacity) = 0;
+    virtual int add(const uint64_t* keys, const float* vecs, size_t n) = 0;
+    virtual int remove(const uint64_t* keys, size_t n, size_t* removed) = 0;
+    virtual int search(const float* q, size_t nq, size_t k, size_t ef, uint64_t* keys, float* dist,
+                       size_t* counts) = 0;
+    virtual const char* last_error() const { return ""; }
+};
+
+struct ActorConfig {
+    size_t reserve_increment = 1000000;  // RESERVE_INCREMENT, usearch.rs:63
+    size_t reserve_threshold = 333333;   // RESERVE_THRESHOLD = increment / 3, :67
+    size_t max_batch = 65536;            // messages drained per worker wake-up
+    uint32_t max_wait_us = 0;            // optional coalescing window (0: natural batching)
+};
+
+struct ActorCounters {
+    uint64_t messages = 0, writes = 0, anns = 0, counts = 0;
+    uint64_t add_calls = 0, remove_calls = 0, search_calls = 0, reserve_calls = 0;
+    uint64_t add_errors = 0, remove_errors = 0, search_errors = 0;
+    uint64_t max_search_batch = 0, max_add_batch = 0;
+};
+
+class Actor {
+  public:
+    enum Kind { ADD, REMOVE, ANN, COUNT, FLUSH };
+
+    // completion of a blocking message (Ann / Count / Flush)
+    struct Waiter {
+        std::mutex m;
+        std::condition_variable cv;
+        bool done = false;
+        int rc = 0;
+        uint64_t* keys = nullptr;
+        float* dist = nullptr;
+        size_t count = 0;  // Ann: results written; Count: live size
+        std::string err;   // backend message when rc != 0
+        void finish(int r) {
+            std::lock_guard<std::mutex> lk(m);
+            rc = r;
+            done = true;
+            cv.notify_all();
+        }
+        int wait() {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return done; });
+            return rc;
+        }
+    };
+
+    struct Msg {
+        Kind kind;
+        uint64_t key = 0;
+        size_t k = 0;
+        std::vector<float> vec;
+        Waiter* w = nullptr;
+    };
+
+    Actor(std::unique_ptr<ActorBackend> be, const ActorConfig& cfg) : be_(std::move(be)), cfg_(cfg) {
+        if (cfg_.max_batch == 0) cfg_.max_batch = 1;
+        worker_ = std::thread([this] { run(); });
+    }
+
+    ~Actor() {
+        {
+            std::lock_guard<std::mutex> lk(qm_);
+            stop_ = true;
+        }
+        qcv_.notify_all();
+        worker_.join();
+    }
+
+    // initial reservation, usearch.rs:99
+    int init() { return be_->reserve(std::max(be_->capacity(), cfg_.reserve_increment)); }
+
+    size_t dimensions() const { return be_->dimensions(); }
+
+    // Index::AddOrReplace — fire and forget, like the reference's channel send
+    void add_or_replace(uint64_t key, const float* vec) {
+        Msg m;
+        m.kind = ADD;
+        m.key = key;
+        m.vec.assign(vec, vec + be_->dimensions());
+        push(std::move(m));
+    }
+
+    // Index::Remove
+    void remove(uint64_t key) {
+        Msg m;
+        m.kind = REMOVE;
+        m.key = key;
+        push(std::move(m));
+    }
+
+    // Index::Ann — blocks until the batched search that contains it finishes.
+    // Dimension check first (usearch.rs:259-272); k >= 1 (Limit is NonZero).
+    int ann(const float* q, size_t dims, size_t k, uint64_t* keys, float* dist, size_t* count,
+            std::string* err = nullptr) {
+        if (k == 0 || dims != be_->dimensions()) return 1;  // VSG_EINVAL
+        Waiter w;
+        w.keys = keys;
+        w.dist = dist;
+        Msg m;
+        m.kind = ANN;
+        m.k = k;
+        m.vec.assign(q, q + dims);
+        m.w = &w;
+        push(std::move(m));
+        const int rc = w.wait();
+        if (count) *count = w.count;
+        if (err) *err = w.err;
+        return rc;
+    }
+
+    // Index::Count
+    int count(size_t* out) {
+        Waiter w;
+        Msg m;
+        m.kind = COUNT;
+        m.w = &w;
+        push(std::move(m));
+        const int rc = w.wait();
+        if (out) *out = w.count;
+        return rc;
+    }
+
+    // wait until every message submitted before this call has been applied
+    int flush() {
+        Waiter w;
+        Msg m;
+        m.kind = FLUSH;
+        m.w = &w;
+        push(std::move(m));
+        return w.wait();
+    }
+
+    ActorCounters counters() const {
+        std::lock_guard<std::mutex> lk(cm_);
+        return ctr_;
+    }
+
+  private:
+    void push(Msg&& m) {
+        {
+            std::lock_guard<std::mutex> lk(qm_);
+            q_.push_back(std::move(m));
+        }
+        qcv_.notify_one();
+    }
+
+    void run() {
+        std::vector<Msg> batch;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(qm_);
+                qcv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty() && stop_) return;
+                if (cfg_.max_wait_us && q_.size() < cfg_.max_batch && !stop_) {
+                    qcv_.wait_for(lk, std::chrono::microseconds(cfg_.max_wait_us),
+                                  [&] { return stop_ || q_.size() >= cfg_.max_batch; });
+                }
+                const size_t n = std::min(q_.size(), cfg_.max_batch);
+                batch.clear();
+                batch.reserve(n);
+                for (size_t i = 0; i < n; ++i) {
+                    batch.push_back(std::move(q_.front()));
+                    q_.pop_front();
+                }
+            }
+            process(batch);
+        }
+    }
+
+    void process(std::vector<Msg>& b) {
+        {
+            std::lock_guard<std::mutex> lk(cm_);
+            ctr_.messages += b.size();
+        }
+        size_t i = 0;
+        while (i < b.size()) {
+            size_t j = i;
+            if (b[i].kind == ADD || b[i].kind == REMOVE) {
+                while (j < b.size() && (b[j].kind == ADD || b[j].kind == REMOVE)) ++j;
+                writes(b, i, j);
+            } else if (b[i].kind == ANN) {
+                while (j < b.size() && b[j].kind == ANN) ++j;
+                anns(b, i, j);
+            } else {
+                if (b[i].kind == COUNT) {
+                    std::lock_guard<std::mutex> lk(cm_);
+                    ctr_.counts++;
+                }
+                b[i].w->count = be_->size();
+                b[i].w->finish(0);
+                j = i + 1;
+            }
+            i = j;
+        }
+    }
+
+    // ---------------------------------------------------------------- writes --
+    // A run of AddOrReplace / Remove messages in FIFO order becomes segments of
+    // one batched remove (keys to drop: explicit removes and the live key of a
+    // replace) followed by one batched add.  A key seen twice closes the
+    // segment, so every key's messages apply in order.
+    struct WriteSeg {
+        std::vector<uint64_t> rm, add;
+        std::vector<float> vecs;
+        std::unordered_set<uint64_t> touched;
+        void clear() {
+            rm.clear();
+            add.clear();
+            vecs.clear();
+            touched.clear();
+        }
+    };
+
+    void writes(std::vector<Msg>& b, size_t i0, size_t i1) {
+        WriteSeg s;
+        const size_t d = be_->dimensions();
+        {
+            std::lock_guard<std::mutex> lk(cm_);
+            ctr_.writes += i1 - i0;
+        }
+        for (size_t i = i0; i < i1; ++i) {
+            const Msg& m = b[i];
+            if (s.touched.count(m.key)) apply(s);
+            s.touched.insert(m.key);
+            if (m.kind == REMOVE) {
+                s.rm.push_back(m.key);
+            } else {
+                if (be_->contains(m.key)) s.rm.push_back(m.key);  // replace, usearch.rs:214-219
+                s.add.push_back(m.key);
+                s.vecs.insert(s.vecs.end(), m.vec.begin(), m.vec.begin() + d);
+            }
+        }
+        apply(s);
+    }
+
+    void apply(WriteSeg& s) {
+        if (!s.rm.empty()) {
+            size_t removed = 0;
+            const int rc = be_->remove(s.rm.data(), s.rm.size(), &removed);
+            std::lock_guard<std::mutex> lk(cm_);
+            ctr_.remove_calls++;
+            if (rc) ctr_.remove_errors += s.rm.size();
+        }
+        if (!s.add.empty()) {
+            // usearch.rs:200-212 as if the batch's vectors arrived one by one:
+            // the last one still finds free >= threshold before its add
+            int rc = 0;
+            const size_t n = s.add.size();
+            while (rc == 0 && be_->capacity() - be_->size() < cfg_.reserve_threshold + n - 1) {
+                rc = be_->reserve(be_->capacity() + cfg_.reserve_increment);
+                std::lock_guard<std::mutex> lk(cm_);
+                ctr_.reserve_calls++;
+            }
+            if (rc == 0) rc = be_->add(s.add.data(), s.vecs.data(), s.add.size());
+            std::lock_guard<std::mutex> lk(cm_);
+            ctr_.add_calls++;
+            ctr_.max_add_batch = std::max<uint64_t>(ctr_.max_add_batch, s.add.size());
+            if (rc) ctr_.add_errors += s.add.size();
+        }
+        s.clear();
+    }
+
+    // ------------------------------------------------------------------ anns --
+    void anns(std::vector<Msg>& b, size_t i0, size_t i1) {
+        const size_t d = be_->dimensions();
+        const size_t ef0 = be_->expansion_search();
+        {
+            std::lock_guard<std::mutex> lk(cm_);
+            ctr_.anns += i1 - i0;
+        }
+        // group by effective ef so batching cannot change any result
+        std::unordered_map<size_t, std::vector<size_t>> groups;
+        std::vector<size_t> order;
+        for (size_t i = i0; i < i1; ++i) {
+            const size_t e = std::max(ef0, b[i].k);
+            auto it = groups.find(e);
+            if (it == groups.end()) {
+                order.push_back(e);
+                groups[e].push_back(i);
+            } else {
+                it->second.push_back(i);
+            }
+        }
+        std::vector<float> qs;
+        std::vector<uint64_t> keys;
+        std::vector<float> dist;
+        std::vector<size_t> counts;
+        for (size_t e : order) {
+            const std::vector<size_t>& g = groups[e];
+            size_t kmax = 0;
+            for (size_t i : g) kmax = std::max(kmax, b[i].k);
+            qs.resize(g.size() * d);
+            for (size_t r = 0; r < g.size(); ++r) std::memcpy(&qs[r * d], b[g[r]].vec.data(), d * 4);
+            keys.resize(g.size() * kmax);
+            dist.resize(g.size() * kmax);
+            counts.resize(g.size());
+            const int rc = be_->search(qs.data(), g.size(), kmax, e, keys.data(), dist.data(), counts.data());
+            {
+                std::lock_guard<std::mutex> lk(cm_);
+                ctr_.search_calls++;
+                ctr_.max_search_batch = std::max<uint64_t>(ctr_.max_search_batch, g.size());
+                if (rc) ctr_.search_errors += g.size();
+            }
+            for (size_t r = 0; r < g.size(); ++r) {
+                Msg& m = b[g[r]];
+                if (rc == 0) {
+                    const size_t c = std::min(counts[r], m.k);
+                    std::memcpy(m.w->keys, &keys[r * kmax], c * 8);
+                    std::memcpy(m.w->dist, &dist[r * kmax], c * 4);
+                    for (size_t t = c; t < m.k; ++t) {
+                        m.w->keys[t] = ~0ull;
+                        m.w->dist[t] = __builtin_inff();
+                    }
+                    m.w->count = c;
+                } else {
+                    m.w->err = be_->last_error();
+                }
+                m.w->finish(rc);
+            }
+        }
+    }
+
+    std::unique_ptr<ActorBackend> be_;
+    ActorConfig cfg_;
+    std::mutex qm_;
+    std::condition_variable qcv_;
+    std::deque<Msg> q_;
+    bool stop_ = false;
+    mutable std::mutex cm_;
+    ActorCounters ctr_;
+    std::thread worker_;
+};
+
+}  // namespace vsg

@@ -37,6 +37,11 @@ static int fail(int code, const std::string& msg) {
     return code;
 }
 
+namespace vsg {
+// shared by the other C-ABI translation units (vsg_actor.cpp)
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+}
+
 #define HIP_TRY(expr)                                                                        \
     do {                                                                                     \
         hipError_t e__ = (expr);                                                             \
@@ -89,6 +94,40 @@ double env_double(const char* name, double dflt) {
 
 }  // namespace
 
+// Reusable context of one host-buffer search call: a stream, pinned staging
+// and device buffers that only grow.  Pooled per index so concurrent callers
+// (and the actor's worker) pay no stream creation / pageable copies per call.
+struct SearchCtx {
+    hipStream_t s = nullptr;
+    uint8_t* pin = nullptr;  // pinned: queries in, then keys | dist | counts out
+    size_t pin_cap = 0;
+    uint8_t* dev = nullptr;  // device: queries | keys | dist | counts
+    size_t dev_cap = 0;
+    ~SearchCtx() {
+        if (pin) (void)hipHostFree(pin);
+        if (dev) (void)hipFree(dev);
+        if (s) (void)hipStreamDestroy(s);
+    }
+};
+
+// Device scratch of one search call (prepared queries, per-block partial
+// top-k lists).  Pooled per index and reused in stream order: a call on
+// stream S waits for the previous user's completion event before touching it.
+// (Stream-ordered hipMallocAsync blocks were not used: with the ROCm 7.2
+// runtime a reused >64 MiB block was seen to hold stale data past its first
+// 64 MiB while the next call's kernels ran -- tools/actor_load reproduces it.)
+struct Workspace {
+    uint8_t* base = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+    ~Workspace() {
+        if (pending) (void)hipEventSynchronize(done);
+        if (base) (void)hipFree(base);
+        if (done) (void)hipEventDestroy(done);
+    }
+};
+
 struct vsg_index {
     vsg_index_options_t opt{};
     int dim = 0;
@@ -133,6 +172,11 @@ struct vsg_index {
 
     mutable std::shared_mutex mu;
     int reverse_grid = 1 << 20;
+    std::mutex ctx_mu;
+    std::vector<SearchCtx*> ctx_free;  // idle search contexts
+    std::vector<Workspace*> ws_free;   // idle device scratch (guarded by ctx_mu)
+    uint32_t* d_rm = nullptr;          // remove(): slot list (writer side)
+    size_t rm_cap = 0;
 
     DevGraph graph() const {
         DevGraph g;
@@ -149,6 +193,11 @@ struct vsg_index {
 };
 
 static void free_dev(vsg_index* h) {
+    for (SearchCtx* c : h->ctx_free) delete c;
+    h->ctx_free.clear();
+    for (Workspace* w : h->ws_free) delete w;
+    h->ws_free.clear();
+    hipFree(h->d_rm);
     hipFree(h->d_vecs);
     hipFree(h->d_adj0);
     hipFree(h->d_upper_off);
@@ -583,16 +632,73 @@ int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_r
         slots.push_back(slot);
     }
     if (!slots.empty()) {
-        uint32_t* d = nullptr;
-        HIP_TRY(hipMallocAsync((void**)&d, slots.size() * 4, h->stream));
-        HIP_TRY(hipMemcpyAsync(d, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(launch_set_flags(h->d_flags, d, slots.size(), 1, h->stream));
-        HIP_TRY(hipFreeAsync(d, h->stream));
+        int rc = ensure_buf(&h->d_rm, h->rm_cap, slots.size());
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(h->d_rm, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(launch_set_flags(h->d_flags, h->d_rm, slots.size(), 1, h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));
     }
     h->live -= slots.size();
     if (n_removed) *n_removed = slots.size();
     return VSG_OK;
+}
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int ws_acquire(vsg_index* h, size_t bytes, hipStream_t s, Workspace** out) {
+    Workspace* w = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(h->ctx_mu);
+        // smallest idle workspace that fits, else the largest (grown below)
+        const size_t none = h->ws_free.size();
+        size_t fit = none, big = none;
+        for (size_t i = 0; i < none; ++i) {
+            const size_t c = h->ws_free[i]->cap;
+            if (c >= bytes && (fit == none || c < h->ws_free[fit]->cap)) fit = i;
+            if (big == none || c > h->ws_free[big]->cap) big = i;
+        }
+        const size_t best = fit != none ? fit : big;
+        if (best < h->ws_free.size()) {
+            w = h->ws_free[best];
+            h->ws_free.erase(h->ws_free.begin() + (long)best);
+        }
+    }
+    if (!w) {
+        w = new Workspace;
+        if (hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess) {
+            delete w;
+            return fail(VSG_EDEVICE, "hipEventCreate failed");
+        }
+    }
+    if (w->cap < bytes) {
+        if (w->pending) (void)hipEventSynchronize(w->done);
+        w->pending = false;
+        if (w->base) (void)hipFree(w->base);
+        w->base = nullptr;
+        const size_t want = std::max(bytes, w->cap * 2);
+        w->cap = 0;
+        if (hipMalloc((void**)&w->base, want) != hipSuccess) {
+            delete w;
+            return fail(VSG_ENOMEM, "search workspace");
+        }
+        w->cap = want;
+    } else if (w->pending) {
+        const hipError_t e = hipStreamWaitEvent(s, w->done, 0);
+        if (e != hipSuccess) {
+            std::lock_guard<std::mutex> lk(h->ctx_mu);
+            h->ws_free.push_back(w);
+            return fail(VSG_EDEVICE, std::string("hipStreamWaitEvent: ") + hipGetErrorString(e));
+        }
+    }
+    *out = w;
+    return VSG_OK;
+}
+
+static void ws_release(vsg_index* h, Workspace* w, hipStream_t s) {
+    w->pending = hipEventRecord(w->done, s) == hipSuccess;
+    if (!w->pending) (void)hipStreamSynchronize(s);
+    std::lock_guard<std::mutex> lk(h->ctx_mu);
+    h->ws_free.push_back(w);
 }
 
 static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, size_t k, size_t ef,
@@ -606,23 +712,37 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
     const size_t mfma_min = (size_t)env_double("VSG_EXACT_MFMA_MIN", 32);
     const bool use_mfma = exact && h->st == ST_F32 && k <= 16 && (h->row_bytes / 4) % 32 == 0 &&
                           nq >= mfma_min && h->slots > 0 && env_double("VSG_EXACT_MFMA", 1) != 0;
-    uint8_t* qp = nullptr;
-    float* qsq = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&qp, nq * h->row_bytes, s));
-    if (use_mfma) HIP_TRY(hipMallocAsync((void**)&qsq, nq * 4, s));
-    HIP_TRY(launch_prepare(h->st, q_dev, nq, h->dim, h->normalize, qp, h->row_bytes, s, qsq));
+    // plan: partial-list shapes, then one scratch block for everything
+    const size_t slots = h->slots;
+    int qtiles = 0, kmax = 0, nparts = 0, nblocks = 1, rpb = 1;
+    size_t splits = 0, tps = 0, np = 0;
     if (use_mfma) {
-        const int qtiles = (int)((nq + MFMA_BQ - 1) / MFMA_BQ);
-        const size_t ntiles = (h->slots + MFMA_BR - 1) / MFMA_BR;
-        size_t splits = std::min<size_t>(ntiles, std::max<size_t>(1, (1024 + qtiles - 1) / qtiles));
-        const size_t tps = (ntiles + splits - 1) / splits;
+        qtiles = (int)((nq + MFMA_BQ - 1) / MFMA_BQ);
+        const size_t ntiles = (slots + MFMA_BR - 1) / MFMA_BR;
+        splits = std::min<size_t>(ntiles, std::max<size_t>(1, (1024 + qtiles - 1) / qtiles));
+        tps = (ntiles + splits - 1) / splits;
         splits = (ntiles + tps - 1) / tps;
-        const int kmax = 16, nparts = (int)splits * 4;
-        float* pd = nullptr;
-        uint32_t* pi = nullptr;
-        const size_t np = nq * (size_t)nparts * kmax;
-        HIP_TRY(hipMallocAsync((void**)&pd, np * 4, s));
-        HIP_TRY(hipMallocAsync((void**)&pi, np * 4, s));
+        kmax = 16;
+        nparts = (int)splits * 4;
+        np = nq * (size_t)nparts * kmax;
+    } else if (exact) {
+        // grid.y = row blocks (<= 65535 per dimension)
+        nblocks = (int)std::min<size_t>(32768, std::max<size_t>(1, (slots + 4095) / 4096));
+        rpb = (int)((slots + nblocks - 1) / nblocks);
+        if (slots == 0) nblocks = 1;
+        np = nq * (size_t)nblocks * k;
+    }
+    const size_t qp_b = align256(nq * h->row_bytes), qsq_b = use_mfma ? align256(nq * 4) : 0,
+                 part_b = align256(np * 4);
+    Workspace* ws = nullptr;
+    int rc = ws_acquire(h, qp_b + qsq_b + 2 * part_b, s, &ws);
+    if (rc) return rc;
+    uint8_t* qp = ws->base;
+    float* qsq = use_mfma ? reinterpret_cast<float*>(ws->base + qp_b) : nullptr;
+    float* pd = reinterpret_cast<float*>(ws->base + qp_b + qsq_b);
+    uint32_t* pi = reinterpret_cast<uint32_t*>(ws->base + qp_b + qsq_b + part_b);
+    hipError_t err = launch_prepare(h->st, q_dev, nq, h->dim, h->normalize, qp, h->row_bytes, s, qsq);
+    if (err == hipSuccess && use_mfma) {
         MfmaExactParams mp{};
         mp.vecs = reinterpret_cast<const float*>(h->d_vecs);
         mp.sqnorm = h->d_sqnorm;
@@ -630,7 +750,7 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         mp.qsqnorm = qsq;
         mp.row_floats = (int)(h->row_bytes / 4);
         mp.nq = (int)nq;
-        mp.nslots = h->slots;
+        mp.nslots = slots;
         mp.flags = h->d_flags;
         mp.qtiles = qtiles;
         mp.splits = (int)splits;
@@ -638,23 +758,22 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         mp.kmax = kmax;
         mp.part_d = pd;
         mp.part_i = pi;
-        HIP_TRY(launch_mfma_exact(h->mk, mp, s));
-        MergeParams gp{};
-        gp.part_d = pd;
-        gp.part_i = pi;
-        gp.nq = (int)nq;
-        gp.parts = nparts;
-        gp.k = (int)k;
-        gp.kin = kmax;
-        gp.keys = h->d_keys;
-        gp.out_keys = ok;
-        gp.out_dist = od;
-        gp.out_counts = oc;
-        HIP_TRY(launch_merge_parts(gp, s));
-        HIP_TRY(hipFreeAsync(pd, s));
-        HIP_TRY(hipFreeAsync(pi, s));
-        HIP_TRY(hipFreeAsync(qsq, s));
-    } else if (!exact) {
+        err = launch_mfma_exact(h->mk, mp, s);
+        if (err == hipSuccess) {
+            MergeParams gp{};
+            gp.part_d = pd;
+            gp.part_i = pi;
+            gp.nq = (int)nq;
+            gp.parts = nparts;
+            gp.k = (int)k;
+            gp.kin = kmax;
+            gp.keys = h->d_keys;
+            gp.out_keys = ok;
+            gp.out_dist = od;
+            gp.out_counts = oc;
+            err = launch_merge_parts(gp, s);
+        }
+    } else if (err == hipSuccess && !exact) {
         size_t e = ef ? ef : (size_t)h->ef;
         e = std::max(e, k);
         if (e > 1024) e = 1024;
@@ -680,18 +799,8 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
             const int factor = (int)env_double("VSG_SEARCH_HASH_FACTOR", wide ? 12 : 6);
             p.hash_size = std::max(hash_size_for(p.ef, factor), wide ? 2048 : 1024);
         }
-        HIP_TRY(launch_search(h->st, h->mk, p, s));
-    } else {
-        const size_t slots = h->slots;
-        // grid.y = row blocks (<= 65535 per dimension)
-        int nblocks = (int)std::min<size_t>(32768, std::max<size_t>(1, (slots + 4095) / 4096));
-        const int rpb = (int)((slots + nblocks - 1) / nblocks);
-        if (slots == 0) nblocks = 1;
-        float* pd = nullptr;
-        uint32_t* pi = nullptr;
-        const size_t np = nq * (size_t)nblocks * k;
-        HIP_TRY(hipMallocAsync((void**)&pd, np * 4, s));
-        HIP_TRY(hipMallocAsync((void**)&pi, np * 4, s));
+        err = launch_search(h->st, h->mk, p, s);
+    } else if (err == hipSuccess) {
         ExactParams ep{};
         ep.vecs = h->d_vecs;
         ep.row_bytes = h->row_bytes;
@@ -705,27 +814,83 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         ep.flags = h->d_flags;
         ep.part_d = pd;
         ep.part_i = pi;
-        if (slots > 0) {
-            HIP_TRY(launch_exact(h->st, h->mk, ep, s));
-        } else {
-            HIP_TRY(hipMemsetAsync(pi, 0xFF, np * 4, s));
+        err = slots > 0 ? launch_exact(h->st, h->mk, ep, s) : hipMemsetAsync(pi, 0xFF, np * 4, s);
+        if (err == hipSuccess) {
+            MergeParams mp{};
+            mp.part_d = pd;
+            mp.part_i = pi;
+            mp.nq = (int)nq;
+            mp.parts = nblocks;
+            mp.k = (int)k;
+            mp.keys = h->d_keys;
+            mp.out_keys = ok;
+            mp.out_dist = od;
+            mp.out_counts = oc;
+            err = launch_merge_parts(mp, s);
         }
-        MergeParams mp{};
-        mp.part_d = pd;
-        mp.part_i = pi;
-        mp.nq = (int)nq;
-        mp.parts = nblocks;
-        mp.k = (int)k;
-        mp.keys = h->d_keys;
-        mp.out_keys = ok;
-        mp.out_dist = od;
-        mp.out_counts = oc;
-        HIP_TRY(launch_merge_parts(mp, s));
-        HIP_TRY(hipFreeAsync(pd, s));
-        HIP_TRY(hipFreeAsync(pi, s));
     }
-    HIP_TRY(hipFreeAsync(qp, s));
+    ws_release(h, ws, s);
+    if (err != hipSuccess) return fail(VSG_EDEVICE, std::string("search launch: ") + hipGetErrorString(err));
     return VSG_OK;
+}
+
+static SearchCtx* ctx_acquire(vsg_index* h) {
+    {
+        std::lock_guard<std::mutex> lk(h->ctx_mu);
+        if (!h->ctx_free.empty()) {
+            SearchCtx* c = h->ctx_free.back();
+            h->ctx_free.pop_back();
+            return c;
+        }
+    }
+    SearchCtx* c = new SearchCtx;
+    if (hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+static void ctx_release(vsg_index* h, SearchCtx* c) {
+    std::lock_guard<std::mutex> lk(h->ctx_mu);
+    h->ctx_free.push_back(c);
+}
+
+static int ctx_reserve(SearchCtx* c, size_t pin_bytes, size_t dev_bytes) {
+    if (pin_bytes > c->pin_cap) {
+        if (c->pin) HIP_TRY(hipHostFree(c->pin));
+        c->pin = nullptr;
+        c->pin_cap = 0;
+        const size_t want = std::max(pin_bytes, c->pin_cap * 2);
+        // coherent (snooped) pinned memory: the buffer is written and read by
+        // the CPU around the DMA; a non-coherent mapping lets the copy engine
+        // read lines still dirty in the CPU caches (seen as stale query rows)
+        HIP_TRY(hipHostMalloc((void**)&c->pin, want, hipHostMallocCoherent));
+        c->pin_cap = want;
+    }
+    if (dev_bytes > c->dev_cap) {
+        if (c->dev) HIP_TRY(hipFree(c->dev));
+        c->dev = nullptr;
+        c->dev_cap = 0;
+        const size_t want = std::max(dev_bytes, c->dev_cap * 2);
+        HIP_TRY(hipMalloc((void**)&c->dev, want));
+        c->dev_cap = want;
+    }
+    return VSG_OK;
+}
+
+// Host<->device copies of the pinned staging buffer in <= 16 MiB pieces.  One
+// hipMemcpyAsync above 64 MiB was seen to complete out of order with the
+// kernels that follow it on the stream (ROCm 7.2 runtime, MI355X; rows past
+// the 64 MiB mark arrived late) -- tools/actor_load reproduces it.
+static hipError_t copy_chunked(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+    const size_t CH = (size_t)16 << 20;
+    for (size_t off = 0; off < bytes; off += CH) {
+        const hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, static_cast<const uint8_t*>(src) + off,
+                                            std::min(CH, bytes - off), kind, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
@@ -735,46 +900,38 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
     if (nq == 0) return VSG_OK;
     std::shared_lock<std::shared_mutex> lk(h->mu);
     DeviceGuard dg(h->device);
-    hipStream_t s;
-    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    float* dq = nullptr;
-    uint64_t* dk = nullptr;
-    float* dd = nullptr;
-    uint32_t* dc = nullptr;
-    int rc = VSG_OK;
-    std::vector<uint32_t> counts(nq);
-    do {
-        if (hipMallocAsync((void**)&dq, nq * h->dim * 4, s) != hipSuccess ||
-            hipMallocAsync((void**)&dk, nq * k * 8, s) != hipSuccess ||
-            hipMallocAsync((void**)&dd, nq * k * 4, s) != hipSuccess ||
-            hipMallocAsync((void**)&dc, nq * 4, s) != hipSuccess) {
-            rc = fail(VSG_ENOMEM, "search workspace");
-            break;
-        }
-        if (hipMemcpyAsync(dq, queries, nq * h->dim * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
+    SearchCtx* c = ctx_acquire(h);
+    if (!c) return fail(VSG_EDEVICE, "hipStreamCreate failed");
+    const size_t qb = align256(nq * h->dim * 4), kb = align256(nq * k * 8), db = align256(nq * k * 4),
+                 cb = align256(nq * 4);
+    int rc = ctx_reserve(c, std::max(qb, kb + db + cb), qb + kb + db + cb);
+    if (rc == VSG_OK) {
+        uint8_t* dq = c->dev;
+        uint64_t* dk = reinterpret_cast<uint64_t*>(c->dev + qb);
+        float* dd = reinterpret_cast<float*>(c->dev + qb + kb);
+        uint32_t* dc = reinterpret_cast<uint32_t*>(c->dev + qb + kb + db);
+        std::memcpy(c->pin, queries, nq * h->dim * 4);
+        if (copy_chunked(dq, c->pin, nq * h->dim * 4, hipMemcpyHostToDevice, c->s) != hipSuccess) {
             rc = fail(VSG_EDEVICE, "H2D queries");
-            break;
+        } else {
+            rc = search_device_locked(h, reinterpret_cast<float*>(dq), nq, k, ef, dk, dd, dc, c->s, exact);
         }
-        rc = search_device_locked(h, dq, nq, k, ef, dk, dd, dc, s, exact);
-        if (rc) break;
-        if (hipMemcpyAsync(out_keys, dk, nq * k * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(out_dist, dd, nq * k * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipMemcpyAsync(counts.data(), dc, nq * 4, hipMemcpyDeviceToHost, s) != hipSuccess) {
+        // results land in the pinned buffer (after the queries were consumed)
+        if (rc == VSG_OK && copy_chunked(c->pin, dk, kb + db + cb, hipMemcpyDeviceToHost, c->s) != hipSuccess)
             rc = fail(VSG_EDEVICE, "D2H results");
-            break;
+        const hipError_t e = hipStreamSynchronize(c->s);
+        if (rc == VSG_OK && e != hipSuccess) rc = fail(VSG_EDEVICE, std::string("search: ") + hipGetErrorString(e));
+        if (rc == VSG_OK) {
+            std::memcpy(out_keys, c->pin, nq * k * 8);
+            std::memcpy(out_dist, c->pin + kb, nq * k * 4);
+            if (out_counts) {
+                const uint32_t* cnt = reinterpret_cast<const uint32_t*>(c->pin + kb + db);
+                for (size_t i = 0; i < nq; ++i) out_counts[i] = cnt[i];
+            }
         }
-    } while (0);
-    if (dq) hipFreeAsync(dq, s);
-    if (dk) hipFreeAsync(dk, s);
-    if (dd) hipFreeAsync(dd, s);
-    if (dc) hipFreeAsync(dc, s);
-    hipError_t e = hipStreamSynchronize(s);
-    hipStreamDestroy(s);
-    if (rc) return rc;
-    if (e != hipSuccess) return fail(VSG_EDEVICE, std::string("search: ") + hipGetErrorString(e));
-    if (out_counts)
-        for (size_t i = 0; i < nq; ++i) out_counts[i] = counts[i];
-    return VSG_OK;
+    }
+    ctx_release(h, c);
+    return rc;
 }
 
 int vsg_index_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
@@ -932,13 +1089,17 @@ int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t m
     if (kind < 0 || kind > 3 || dim == 0) return fail(VSG_EINVAL, "bad datagen arguments");
     hipStream_t s = (hipStream_t)stream;
     float *w = nullptr, *c = nullptr;
-    if (kind == 0 || kind == 3) {
-        HIP_TRY(hipMallocAsync((void**)&w, 64 * dim * 4, s));
-        HIP_TRY(hipMallocAsync((void**)&c, 1024 * 64 * 4, s));
+    if (kind == 0 || kind == 3) {  // latent model scratch (small; freed after the stream drains)
+        HIP_TRY(hipMalloc((void**)&w, 64 * dim * 4));
+        HIP_TRY(hipMalloc((void**)&c, 1024 * 64 * 4));
     }
-    HIP_TRY(launch_datagen(kind, n, dim, seed, model_seed, start_row, out, w, c, s));
-    if (w) HIP_TRY(hipFreeAsync(w, s));
-    if (c) HIP_TRY(hipFreeAsync(c, s));
+    const hipError_t e = launch_datagen(kind, n, dim, seed, model_seed, start_row, out, w, c, s);
+    if (w) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(w);
+        (void)hipFree(c);
+    }
+    if (e != hipSuccess) return fail(VSG_EDEVICE, std::string("datagen: ") + hipGetErrorString(e));
     return VSG_OK;
 }
 

@@ -68,6 +68,23 @@ class Stats(C.Structure):
     ]
 
 
+class ActorOptions(C.Structure):
+    _fields_ = [
+        ("index", Options),
+        ("reserve_increment", C.c_uint64),
+        ("reserve_threshold", C.c_uint64),
+        ("max_batch", C.c_uint32),
+        ("max_wait_us", C.c_uint32),
+    ]
+
+
+class ActorCounters(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in (
+        "messages", "writes", "anns", "counts", "add_calls", "remove_calls", "search_calls",
+        "reserve_calls", "add_errors", "remove_errors", "search_errors", "max_search_batch",
+        "max_add_batch")]
+
+
 _lib = None
 
 
@@ -117,6 +134,15 @@ def lib() -> C.CDLL:
         "vsg_index_import": (C.c_int, [P, sz, P, P, P, P, P, P, P, sz, u32, C.c_int]),
         "vsg_datagen_device": (C.c_int, [C.c_int, sz, sz, u64, u64, sz, P, P]),
         "vsg_sample_level": (C.c_int, [u64, u64, u32]),
+        "vsg_actor_new": (C.c_int, [C.POINTER(ActorOptions), C.POINTER(P)]),
+        "vsg_actor_free": (None, [P]),
+        "vsg_actor_add_or_replace": (C.c_int, [P, u64, P, sz]),
+        "vsg_actor_remove": (C.c_int, [P, u64]),
+        "vsg_actor_ann": (C.c_int, [P, P, sz, sz, P, P, C.POINTER(sz)]),
+        "vsg_actor_count": (C.c_int, [P, C.POINTER(sz)]),
+        "vsg_actor_flush": (C.c_int, [P]),
+        "vsg_actor_counters": (C.c_int, [P, C.POINTER(ActorCounters)]),
+        "vsg_actor_index": (P, [P]),
         "vsg_last_error": (C.c_char_p, []),
         "vsg_version": (C.c_char_p, []),
     }

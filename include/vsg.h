@@ -160,6 +160,36 @@ int vsg_index_import(vsg_index_t* index, size_t slots, const float* vectors,
                      const uint32_t* adj0, const uint32_t* upper_off, const uint32_t* upper,
                      size_t upper_rows, uint32_t entry, int max_level);
 
+/* Compaction: tombstoned rows (vsg_index_remove) keep
+ * routing the traversal until compaction drops them.  Gathers the live rows in
+ * slot order into a dense image and rebuilds the graph over them on the GPU.
+ * Keys, live size and capacity are unchanged; *n_dropped (optional) = slots
+ * freed.  Takes the writer lock.  usearch compacts through its own
+ * `compact`/`isolate` (not called by the reference, src/index/usearch.rs:235-249). */
+int vsg_index_compact(vsg_index_t* index, size_t* n_dropped);
+
+/* Persistence (the reference rebuilds from a DB scan instead,
+ * src/db_index.rs:213-237).  One file: a 128-byte header (magic "VSGIDX\0\1",
+ * version 1, options, sizes, entry point, FNV-1a-64 checksums) followed by the
+ * HBM image (stored rows, |x|^2, keys, flags, levels, level-0 adjacency,
+ * upper_off, upper rows).  Save writes `path`.tmp then renames.  Load creates a
+ * new index on `device` and verifies sizes and both checksums; a loaded index
+ * answers searches bit-identically to the saved one. */
+typedef struct {
+    vsg_index_options_t options; /* as created (device = the saving device) */
+    uint32_t version;
+    int32_t max_level;
+    uint64_t slots;      /* stored rows, tombstones included */
+    uint64_t live;       /* vsg_index_size() */
+    uint64_t upper_rows;
+    uint64_t file_bytes;
+} vsg_file_info_t;
+
+int vsg_index_save(const vsg_index_t* index, const char* path);
+int vsg_index_load(const char* path, int device, vsg_index_t** out);
+/* header check only (magic, version, header checksum, size); no device needed */
+int vsg_index_file_info(const char* path, vsg_file_info_t* out);
+
 /* Synthetic inputs generated in HBM (vsg/datagen.py formulas): kind 0 =
  * clustered-latent, 1 = iid gaussian, 2 = uint8-valued, 3 = SIFT-like
  * (clustered, ReLU, x48, rounded into 0..255). */

@@ -1,0 +1,126 @@
+"""GPU: compaction and persistence of an index.
+
+Compaction keeps the live set and its slot order, so exact search is
+bit-identical before and after; the rebuilt graph is checked for recall
+against the oracle's exact answers over the live rows.  A saved and reloaded
+index answers bit-identically (HNSW and exact), keeps keys / tombstones /
+capacity growth working, and a damaged file is refused.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import vsg
+from vsg import datagen as G
+
+pytestmark = pytest.mark.gpu
+
+NOKEY = np.uint64(2**64 - 1)
+
+
+def recall(found, truth, k):
+    return float(np.mean([len(set(found[i][:k].tolist()) & set(truth[i][:k].tolist())) / k
+                          for i in range(truth.shape[0])]))
+
+
+@pytest.mark.parametrize("metric,quant", [("l2sq", "f32"), ("ip", "f16"), ("cos", "f32")])
+def test_compact_keeps_exact_answers_and_recall(metric, quant):
+    n, dim = 12000, 64
+    x = G.uint8_valued(n, dim, 81) if metric == "l2sq" else G.clustered(n, dim, *G.config_seeds(1)[::2])
+    q = G.uint8_valued(100, dim, 82) if metric == "l2sq" else G.clustered(100, dim, *G.config_seeds(1)[1:])
+    idx = vsg.Index(dim, metric, quant, 16, 128, 64, seed=3)
+    idx.add(np.arange(n), x)
+    rng = np.random.default_rng(1)
+    dead = rng.choice(n, size=5000, replace=False)
+    assert idx.remove(dead) == 5000
+    before = idx.exact_search(q, 10)
+    assert idx.graph_info()["slots"] == n
+    assert idx.compact() == 5000
+    assert idx.compact() == 0  # nothing left to drop
+    assert idx.size() == n - 5000 and idx.graph_info()["slots"] == n - 5000
+    after = idx.exact_search(q, 10)
+    np.testing.assert_array_equal(before.keys, after.keys)
+    np.testing.assert_array_equal(before.distances, after.distances)
+    live = np.setdiff1d(np.arange(n), dead)
+    assert all(idx.contains(int(k)) for k in live[:50]) and not any(idx.contains(int(k)) for k in dead[:50])
+    m = idx.search(q, 10, 64)
+    assert not np.isin(m.keys, dead).any()
+    assert recall(m.keys, after.keys, 10) >= 0.95
+    if metric == "l2sq":  # oracle over the live rows (integer data: exact distances)
+        ok, od, _ = O.exact_search("l2sq", x[live], q, 10)
+        np.testing.assert_array_equal(after.distances, od)
+        np.testing.assert_array_equal(after.keys, live[ok.astype(np.int64)].astype(np.uint64))
+    # dropped keys can come back; compacted keys can go
+    idx.add(dead[:100], x[dead[:100]])
+    assert idx.remove(live[:10]) == 10
+    m = idx.search(x[dead[:100]], 1, 64)
+    assert (m.keys[:, 0] == dead[:100]).mean() > 0.95
+
+
+def test_compact_everything_and_exact_only():
+    idx = vsg.Index(8, "l2sq")
+    idx.add(np.arange(50), np.random.default_rng(0).standard_normal((50, 8)).astype(np.float32))
+    idx.remove(np.arange(50))
+    assert idx.compact() == 50 and idx.size() == 0
+    m = idx.search(np.zeros((2, 8), np.float32), 3)
+    assert (m.counts == 0).all() and (m.keys == NOKEY).all()
+    idx.add([5], np.ones((1, 8), np.float32))
+    assert int(idx.search(np.zeros((1, 8), np.float32), 1).keys[0, 0]) == 5
+    e = vsg.Index(16, "ip", exact_only=True)
+    xe = G.uint8_valued(500, 16, 3)
+    e.add(np.arange(500), xe)
+    e.remove(np.arange(0, 500, 2))
+    before = e.exact_search(xe[:20], 5)
+    assert e.compact() == 250
+    after = e.exact_search(xe[:20], 5)
+    np.testing.assert_array_equal(before.keys, after.keys)
+
+
+@pytest.mark.parametrize("metric,quant,dim", [("cos", "f32", 768), ("l2sq", "f16", 128), ("ip", "f32", 40)])
+def test_save_load_roundtrip_bitexact(tmp_path, metric, quant, dim):
+    n = 20000
+    bs, qs, ms = G.config_seeds(1)
+    x = G.clustered(n, dim, bs, ms)
+    q = G.clustered(200, dim, qs, ms)
+    a = vsg.Index(dim, metric, quant, 16, 128, 48, seed=9)
+    a.add(np.arange(n) * 3 + 1, x)
+    a.remove(np.arange(0, 600) * 3 + 1)
+    p = tmp_path / "idx.vsg"
+    a.save(p)
+    info = vsg.file_info(p)
+    assert info["slots"] == n and info["live"] == n - 600 and info["dimensions"] == dim
+    assert info["metric"] == metric and info["quantization"] == quant
+    b = vsg.Index.load(p, device=0)
+    assert b.size() == a.size() and b.graph_info() == a.graph_info()
+    for ef in (0, 16, 100):
+        ma, mb = a.search(q, 10, ef), b.search(q, 10, ef)
+        np.testing.assert_array_equal(ma.keys, mb.keys)
+        np.testing.assert_array_equal(ma.distances, mb.distances)
+    ea, eb = a.exact_search(q, 10), b.exact_search(q, 10)
+    np.testing.assert_array_equal(ea.keys, eb.keys)
+    np.testing.assert_array_equal(ea.distances, eb.distances)
+    ga, gb = a.export(), b.export()
+    for k in ("keys", "removed", "levels", "adj0", "upper_off", "upper", "vectors"):
+        np.testing.assert_array_equal(ga[k], gb[k])
+    # the loaded index keeps working: duplicate keys, new rows, removes
+    with pytest.raises(vsg.DuplicateKeyError):
+        b.add([1801], x[1:2])  # key of row 600: live
+    b.add([1], x[0:1])  # key 1 was removed: may come back
+    b.add(np.arange(500) + 10**9, x[:500])
+    assert b.size() == n - 600 + 1 + 500
+    assert b.remove([1, 1801, 1804, 4]) == 3  # key 4 was removed before the save
+
+
+def test_load_rejects_damaged_payload(tmp_path):
+    a = vsg.Index(16, "l2sq")
+    a.add(np.arange(300), G.uint8_valued(300, 16, 4))
+    p = tmp_path / "d.vsg"
+    a.save(p)
+    raw = bytearray(p.read_bytes())
+    raw[200] ^= 0x10  # inside the stored rows
+    p.write_bytes(bytes(raw))
+    with pytest.raises(vsg.VsgError, match="checksum"):
+        vsg.Index.load(p)
+    p.write_bytes(bytes(raw[:-8]))
+    with pytest.raises(vsg.VsgError):
+        vsg.Index.load(p)

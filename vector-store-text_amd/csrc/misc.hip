@@ -101,6 +101,37 @@ hipError_t launch_set_flags(uint8_t* flags, const uint32_t* slots, size_t n, uin
     return hipGetLastError();
 }
 
+// Compaction gather (vsg_index_compact): live slot idx[i] -> row i of the new
+// image.  One wave per row, 16-B vector loads/stores (rows are 16-B multiples).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ vecs,
+                                                          const float* __restrict__ sqnorm,
+                                                          const uint64_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ idx, size_t n,
+                                                          size_t row_bytes, uint8_t* __restrict__ out_vecs,
+                                                          float* __restrict__ out_sq, uint64_t* __restrict__ out_keys) {
+    const int lane = threadIdx.x & 63;
+    const size_t n16 = row_bytes / 16;
+    for (size_t row = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (size_t)gridDim.x * 4) {
+        const size_t src = idx[row];
+        const uint4* a = reinterpret_cast<const uint4*>(vecs + src * row_bytes);
+        uint4* b = reinterpret_cast<uint4*>(out_vecs + row * row_bytes);
+        for (size_t c = lane; c < n16; c += 64) b[c] = a[c];
+        if (lane == 0) {
+            out_sq[row] = sqnorm[src];
+            out_keys[row] = keys[src];
+        }
+    }
+}
+
+hipError_t launch_gather_rows(const uint8_t* vecs, const float* sqnorm, const uint64_t* keys, const uint32_t* idx,
+                              size_t n, size_t row_bytes, uint8_t* out_vecs, float* out_sq, uint64_t* out_keys,
+                              hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(capped_grid(n, 4)), dim3(256), 0, s, vecs, sqnorm, keys, idx, n,
+                       row_bytes, out_vecs, out_sq, out_keys);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- datagen --
 // Same formulas and stream tags as vector-store-text_amd/vsg/datagen.py.
 

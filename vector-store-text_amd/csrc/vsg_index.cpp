@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstddef>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -1081,6 +1083,312 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
         }
     h->entry = entry;
     h->max_level = max_level;
+    return VSG_OK;
+}
+
+// ------------------------------------------------------------ compaction --
+// Tombstoned slots stay in the graph (they route the traversal, like usearch's
+// removed entries) until compaction: the live rows are gathered in slot order
+// into a dense image and the graph is rebuilt over them with the batched GPU
+// build.  Relative slot order is kept, so exact-search ties resolve as before.
+
+int vsg_index_compact(vsg_index_t* h, size_t* n_dropped) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    if (n_dropped) *n_dropped = 0;
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    const size_t s = h->slots;
+    if (s == h->live) return VSG_OK;
+    hipStream_t st = h->stream;
+    std::vector<uint8_t> fl(s);
+    HIP_TRY(hipMemcpyAsync(fl.data(), h->d_flags, s, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<uint32_t> idx;
+    idx.reserve(h->live);
+    for (size_t i = 0; i < s; ++i)
+        if (!(fl[i] & 1)) idx.push_back((uint32_t)i);
+    const size_t n = idx.size();
+    // scratch first: a failed allocation leaves the index untouched
+    uint32_t* d_idx = nullptr;
+    uint8_t* nv = nullptr;
+    float* nsq = nullptr;
+    uint64_t* nk = nullptr;
+    auto release = [&]() {
+        hipFree(d_idx);
+        hipFree(nv);
+        hipFree(nsq);
+        hipFree(nk);
+    };
+    if (n && (dev_alloc(&d_idx, n) != hipSuccess || dev_alloc(&nv, n * h->row_bytes) != hipSuccess ||
+              dev_alloc(&nsq, n) != hipSuccess || dev_alloc(&nk, n) != hipSuccess)) {
+        release();
+        return fail(VSG_ENOMEM, "compaction scratch");
+    }
+    std::vector<uint64_t> keys(n);
+    hipError_t e = hipSuccess;
+    if (n) {
+        e = hipMemcpyAsync(d_idx, idx.data(), n * 4, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = launch_gather_rows(h->d_vecs, h->d_sqnorm, h->d_keys, d_idx, n, h->row_bytes, nv, nsq, nk, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(keys.data(), nk, n * 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(h->d_vecs, nv, n * h->row_bytes, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(h->d_sqnorm, nsq, n * 4, hipMemcpyDeviceToDevice, st);
+    }
+    // drop the old graph
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_adj0, 0xFF, s * h->M0 * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_upper_off, 0xFF, s * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_keys, 0xFF, s * 8, st);
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_flags, 0, s, st);
+    if (e == hipSuccess && h->upper_used) e = hipMemsetAsync(h->d_upper, 0xFF, h->upper_used * h->M * 4, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    release();
+    if (e != hipSuccess) return fail(VSG_EDEVICE, std::string("compaction: ") + hipGetErrorString(e));
+    h->keys = KeyMap();
+    h->slots = 0;
+    h->live = 0;
+    h->upper_used = 0;
+    h->entry = 0xFFFFFFFFu;
+    h->max_level = -1;
+    int rc = map_keys(h, keys.data(), n, 0);
+    if (rc == VSG_OK && n) {
+        rc = insert_slots(h, 0, n, keys.data());
+        if (rc == VSG_OK) HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (rc) return rc;
+    if (n_dropped) *n_dropped = s - n;
+    return VSG_OK;
+}
+
+// ------------------------------------------------------------ persistence --
+// File = FileHeader + payload sections in HBM layout: stored
+// rows (f32/f16, normalised for cos: bit-exact round trip), |x|^2, keys,
+// flags, levels, adj0, upper_off, upper.  FNV-1a-64 over the header and the
+// payload; streamed through a 16 MiB pinned buffer.
+
+}  // extern "C"
+
+namespace {
+
+constexpr char kMagic[8] = {'V', 'S', 'G', 'I', 'D', 'X', 0, 1};
+constexpr uint32_t kFileVersion = 1;
+
+struct FileHeader {
+    char magic[8];
+    uint32_t version;
+    uint32_t header_bytes;
+    vsg_index_options_t opt;
+    uint64_t slots, live, upper_rows, row_bytes;
+    uint32_t M, M0, efc, ef;
+    uint32_t entry;
+    int32_t max_level;
+    uint64_t payload_hash;
+    uint64_t header_hash;  // over every byte above
+};
+static_assert(sizeof(FileHeader) == 128, "file header layout");
+
+struct Fnv {
+    uint64_t h = 0xcbf29ce484222325ull;
+    void update(const void* p, size_t n) {
+        const uint8_t* b = static_cast<const uint8_t*>(p);
+        uint64_t x = h;
+        for (size_t i = 0; i < n; ++i) x = (x ^ b[i]) * 0x100000001b3ull;
+        h = x;
+    }
+};
+
+uint64_t header_hash(const FileHeader& fh) {
+    Fnv f;
+    f.update(&fh, offsetof(FileHeader, header_hash));
+    return f.h;
+}
+
+struct Section {
+    void* dev;
+    size_t bytes;
+};
+
+std::vector<Section> sections(vsg_index* h, size_t slots, size_t upper_rows) {
+    return {{h->d_vecs, slots * h->row_bytes}, {h->d_sqnorm, slots * 4},      {h->d_keys, slots * 8},
+            {h->d_flags, slots},               {nullptr, slots} /* levels */, {h->d_adj0, slots * h->M0 * 4},
+            {h->d_upper_off, slots * 4},       {h->d_upper, upper_rows * h->M * 4}};
+}
+
+size_t payload_bytes(const FileHeader& fh) {
+    const size_t s = fh.slots;
+    return s * fh.row_bytes + s * 4 + s * 8 + s + s + s * fh.M0 * 4 + s * 4 + fh.upper_rows * fh.M * 4;
+}
+
+int read_header(FILE* f, FileHeader& fh, size_t* file_bytes) {
+    if (std::fseek(f, 0, SEEK_END) != 0) return fail(VSG_EINVAL, "cannot seek index file");
+    const long sz = std::ftell(f);
+    std::rewind(f);
+    if (sz < (long)sizeof(FileHeader) || std::fread(&fh, sizeof(fh), 1, f) != 1)
+        return fail(VSG_EINVAL, "not a vsg index file (truncated header)");
+    if (std::memcmp(fh.magic, kMagic, 8) != 0) return fail(VSG_EINVAL, "not a vsg index file (bad magic)");
+    if (fh.version != kFileVersion || fh.header_bytes != sizeof(FileHeader))
+        return fail(VSG_EUNSUPPORTED, "unsupported vsg index file version " + std::to_string(fh.version));
+    if (header_hash(fh) != fh.header_hash) return fail(VSG_EINVAL, "vsg index file header checksum mismatch");
+    if (fh.M0 != 2 * fh.M || fh.M < 2 || fh.M > 32 || fh.live > fh.slots || fh.slots > MAX_SLOTS)
+        return fail(VSG_EINVAL, "vsg index file header is inconsistent");
+    if ((size_t)sz != sizeof(FileHeader) + payload_bytes(fh))
+        return fail(VSG_EINVAL, "vsg index file size does not match its header (truncated?)");
+    if (file_bytes) *file_bytes = (size_t)sz;
+    return VSG_OK;
+}
+
+struct FileCloser {
+    FILE* f;
+    ~FileCloser() {
+        if (f) std::fclose(f);
+    }
+};
+
+struct PinnedBuf {
+    uint8_t* p = nullptr;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+constexpr size_t kIoChunk = (size_t)16 << 20;
+
+}  // namespace
+
+extern "C" {
+
+int vsg_index_save(const vsg_index_t* h, const char* path) {
+    if (!h || !path) return fail(VSG_EINVAL, "null argument");
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    DeviceGuard dg(h->device);
+    vsg_index* ix = const_cast<vsg_index*>(h);
+    FileHeader fh{};
+    std::memcpy(fh.magic, kMagic, 8);
+    fh.version = kFileVersion;
+    fh.header_bytes = sizeof(FileHeader);
+    fh.opt = h->opt;
+    fh.slots = h->slots;
+    fh.live = h->live;
+    fh.upper_rows = h->upper_used;
+    fh.row_bytes = h->row_bytes;
+    fh.M = (uint32_t)h->M;
+    fh.M0 = (uint32_t)h->M0;
+    fh.efc = (uint32_t)h->efc;
+    fh.ef = (uint32_t)h->ef;
+    fh.entry = h->entry;
+    fh.max_level = h->max_level;
+    const std::string tmp = std::string(path) + ".tmp";
+    FileCloser fc{std::fopen(tmp.c_str(), "wb")};
+    if (!fc.f) return fail(VSG_EINVAL, std::string("cannot open ") + tmp + " for writing");
+    // header placeholder, rewritten with the payload hash at the end
+    if (std::fwrite(&fh, sizeof(fh), 1, fc.f) != 1) return fail(VSG_EINVAL, "write failed (header)");
+    PinnedBuf buf;
+    HIP_TRY(hipHostMalloc((void**)&buf.p, kIoChunk, hipHostMallocDefault));
+    Fnv hash;
+    hipStream_t st = h->stream;
+    for (const Section& sec : sections(ix, fh.slots, fh.upper_rows)) {
+        for (size_t off = 0; off < sec.bytes; off += kIoChunk) {
+            const size_t c = std::min(kIoChunk, sec.bytes - off);
+            if (sec.dev) {
+                HIP_TRY(hipMemcpyAsync(buf.p, static_cast<const uint8_t*>(sec.dev) + off, c, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+            } else {
+                std::memcpy(buf.p, reinterpret_cast<const uint8_t*>(h->h_levels.data()) + off, c);
+            }
+            hash.update(buf.p, c);
+            if (std::fwrite(buf.p, 1, c, fc.f) != c) return fail(VSG_EINVAL, "write failed (payload)");
+        }
+    }
+    fh.payload_hash = hash.h;
+    fh.header_hash = header_hash(fh);
+    if (std::fseek(fc.f, 0, SEEK_SET) != 0 || std::fwrite(&fh, sizeof(fh), 1, fc.f) != 1)
+        return fail(VSG_EINVAL, "write failed (header)");
+    if (std::fclose(fc.f) != 0) {
+        fc.f = nullptr;
+        return fail(VSG_EINVAL, "close failed");
+    }
+    fc.f = nullptr;
+    if (std::rename(tmp.c_str(), path) != 0) return fail(VSG_EINVAL, std::string("cannot rename to ") + path);
+    return VSG_OK;
+}
+
+int vsg_index_file_info(const char* path, vsg_file_info_t* out) {
+    if (!path || !out) return fail(VSG_EINVAL, "null argument");
+    FileCloser fc{std::fopen(path, "rb")};
+    if (!fc.f) return fail(VSG_EINVAL, std::string("cannot open ") + path);
+    FileHeader fh;
+    size_t bytes = 0;
+    int rc = read_header(fc.f, fh, &bytes);
+    if (rc) return rc;
+    out->options = fh.opt;
+    out->version = fh.version;
+    out->max_level = fh.max_level;
+    out->slots = fh.slots;
+    out->live = fh.live;
+    out->upper_rows = fh.upper_rows;
+    out->file_bytes = bytes;
+    return VSG_OK;
+}
+
+int vsg_index_load(const char* path, int device, vsg_index_t** out) {
+    if (!path || !out) return fail(VSG_EINVAL, "null argument");
+    *out = nullptr;
+    FileCloser fc{std::fopen(path, "rb")};
+    if (!fc.f) return fail(VSG_EINVAL, std::string("cannot open ") + path);
+    FileHeader fh;
+    int rc = read_header(fc.f, fh, nullptr);
+    if (rc) return rc;
+    vsg_index_options_t o = fh.opt;
+    o.device = device;
+    vsg_index_t* h = nullptr;
+    if ((rc = vsg_index_new(&o, &h))) return rc;
+    struct Owner {
+        vsg_index_t* h;
+        ~Owner() {
+            if (h) vsg_index_free(h);
+        }
+    } own{h};
+    if (h->row_bytes != fh.row_bytes || (uint32_t)h->M != fh.M)
+        return fail(VSG_EINVAL, "vsg index file does not match its options");
+    DeviceGuard dg(h->device);
+    const size_t s = fh.slots;
+    if (s && (rc = reserve_locked(h, s))) return rc;
+    if ((rc = ensure_upper(h, fh.upper_rows))) return rc;
+    std::vector<uint64_t> keys(s);
+    std::vector<uint8_t> flags(s);
+    PinnedBuf buf;
+    HIP_TRY(hipHostMalloc((void**)&buf.p, kIoChunk, hipHostMallocDefault));
+    Fnv hash;
+    hipStream_t st = h->stream;
+    const std::vector<Section> secs = sections(h, s, fh.upper_rows);
+    for (size_t si = 0; si < secs.size(); ++si) {
+        const Section& sec = secs[si];
+        for (size_t off = 0; off < sec.bytes; off += kIoChunk) {
+            const size_t c = std::min(kIoChunk, sec.bytes - off);
+            if (std::fread(buf.p, 1, c, fc.f) != c) return fail(VSG_EINVAL, "read failed (truncated payload)");
+            hash.update(buf.p, c);
+            if (sec.dev) {
+                HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(sec.dev) + off, buf.p, c, hipMemcpyHostToDevice, st));
+                HIP_TRY(hipStreamSynchronize(st));
+            }
+            if (si == 2) std::memcpy(reinterpret_cast<uint8_t*>(keys.data()) + off, buf.p, c);
+            if (si == 3) std::memcpy(flags.data() + off, buf.p, c);
+            if (si == 4) std::memcpy(reinterpret_cast<uint8_t*>(h->h_levels.data()) + off, buf.p, c);
+        }
+    }
+    if (hash.h != fh.payload_hash) return fail(VSG_EINVAL, "vsg index file payload checksum mismatch");
+    h->slots = s;
+    h->upper_used = fh.upper_rows;
+    h->entry = fh.entry;
+    h->max_level = fh.max_level;
+    h->live = 0;
+    h->keys.reserve(fh.live);
+    for (size_t i = 0; i < s; ++i)
+        if (!(flags[i] & 1)) {
+            if (!h->keys.insert(keys[i], (uint32_t)i)) return fail(VSG_EINVAL, "vsg index file has duplicate live keys");
+            h->live++;
+        }
+    if (h->live != fh.live) return fail(VSG_EINVAL, "vsg index file live count mismatch");
+    *out = h;
+    own.h = nullptr;
     return VSG_OK;
 }
 

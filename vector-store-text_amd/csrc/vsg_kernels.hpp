@@ -131,6 +131,10 @@ hipError_t launch_unprepare(Storage st, const uint8_t* in, size_t n, int dim, si
                             float* out, hipStream_t s);
 hipError_t launch_set_flags(uint8_t* flags, const uint32_t* slots, size_t n, uint8_t value,
                             hipStream_t s);
+// rows / |x|^2 / keys of slots idx[0..n) -> dense outputs (compaction)
+hipError_t launch_gather_rows(const uint8_t* vecs, const float* sqnorm, const uint64_t* keys,
+                              const uint32_t* idx, size_t n, size_t row_bytes, uint8_t* out_vecs,
+                              float* out_sq, uint64_t* out_keys, hipStream_t s);
 hipError_t launch_datagen(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed,
                           size_t start_row, float* out, float* scratch_w, float* scratch_c,
                           hipStream_t s);

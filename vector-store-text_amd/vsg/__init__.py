@@ -5,7 +5,7 @@ Product path: libvsg.so (gfx950 HIP kernels behind include/vsg.h), reached
 through ctypes.  No CPU fallback.
 """
 from ._lib import (DuplicateKeyError, VsgError, LIB_PATH, NO_KEY, declared_symbols, lib)  # noqa: F401
-from .index import Index, Matches, datagen_device, merge_topk_device, sample_level  # noqa: F401
+from .index import Index, Matches, datagen_device, file_info, merge_topk_device, sample_level  # noqa: F401
 
 __all__ = ["Index", "Matches", "DuplicateKeyError", "VsgError", "datagen_device",
-           "merge_topk_device", "sample_level", "declared_symbols", "lib", "LIB_PATH", "NO_KEY"]
+           "merge_topk_device", "sample_level", "file_info", "declared_symbols", "lib", "LIB_PATH", "NO_KEY"]

@@ -68,6 +68,18 @@ class Stats(C.Structure):
     ]
 
 
+class FileInfo(C.Structure):
+    _fields_ = [
+        ("options", Options),
+        ("version", C.c_uint32),
+        ("max_level", C.c_int32),
+        ("slots", C.c_uint64),
+        ("live", C.c_uint64),
+        ("upper_rows", C.c_uint64),
+        ("file_bytes", C.c_uint64),
+    ]
+
+
 class ActorOptions(C.Structure):
     _fields_ = [
         ("index", Options),
@@ -132,6 +144,10 @@ def lib() -> C.CDLL:
                                            C.POINTER(u32), C.POINTER(C.c_int)]),
         "vsg_index_export": (C.c_int, [P] * 8),
         "vsg_index_import": (C.c_int, [P, sz, P, P, P, P, P, P, P, sz, u32, C.c_int]),
+        "vsg_index_compact": (C.c_int, [P, C.POINTER(sz)]),
+        "vsg_index_save": (C.c_int, [P, C.c_char_p]),
+        "vsg_index_load": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(P)]),
+        "vsg_index_file_info": (C.c_int, [C.c_char_p, C.POINTER(FileInfo)]),
         "vsg_datagen_device": (C.c_int, [C.c_int, sz, sz, u64, u64, sz, P, P]),
         "vsg_sample_level": (C.c_int, [u64, u64, u32]),
         "vsg_actor_new": (C.c_int, [C.POINTER(ActorOptions), C.POINTER(P)]),

@@ -13,7 +13,12 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import METRICS, NO_KEY, SCALARS, Options, Stats, check, lib
+import os
+
+from ._lib import METRICS, NO_KEY, SCALARS, FileInfo, Options, Stats, check, lib
+
+_METRIC_NAMES = {v: k for k, v in METRICS.items()}
+_SCALAR_NAMES = {v: k for k, v in SCALARS.items()}
 
 
 def _p(a):
@@ -183,6 +188,43 @@ class Index:
                                      _p(a["levels"]), _p(a["adj0"]), _p(a["upper_off"]),
                                      _p(a["upper"]), a["upper"].shape[0], int(g["entry"]),
                                      int(g["max_level"])))
+
+
+    # -- compaction / persistence -------------------------
+    def compact(self) -> int:
+        """Drop tombstoned rows and rebuild the graph over the live ones; returns
+        the number of slots freed."""
+        n = C.c_size_t()
+        check(lib().vsg_index_compact(self._h, C.byref(n)))
+        return n.value
+
+    def save(self, path) -> None:
+        check(lib().vsg_index_save(self._h, os.fsencode(path)))
+
+    @classmethod
+    def load(cls, path, device: int = 0) -> "Index":
+        info = file_info(path)
+        h = C.c_void_p()
+        check(lib().vsg_index_load(os.fsencode(path), int(device), C.byref(h)))
+        self = cls.__new__(cls)
+        self._h = h
+        self.device = device
+        self.dimensions = info["dimensions"]
+        self.metric = info["metric"]
+        self.quantization = info["quantization"]
+        return self
+
+
+def file_info(path) -> dict:
+    """Header of a saved index (no device needed)."""
+    fi = FileInfo()
+    check(lib().vsg_index_file_info(os.fsencode(path), C.byref(fi)))
+    o = fi.options
+    return {"dimensions": o.dimensions, "metric": _METRIC_NAMES[o.metric],
+            "quantization": _SCALAR_NAMES[o.quantization], "connectivity": o.connectivity,
+            "expansion_add": o.expansion_add, "expansion_search": o.expansion_search,
+            "flags": o.flags, "seed": o.seed, "version": fi.version, "max_level": fi.max_level,
+            "slots": fi.slots, "live": fi.live, "upper_rows": fi.upper_rows, "file_bytes": fi.file_bytes}
 
 
 def merge_topk_device(keys_t, dist_t, k, stream=None):

@@ -45,7 +45,11 @@ def test_compact_keeps_exact_answers_and_recall(metric, quant):
     assert all(idx.contains(int(k)) for k in live[:50]) and not any(idx.contains(int(k)) for k in dead[:50])
     m = idx.search(q, 10, 64)
     assert not np.isin(m.keys, dead).any()
-    assert recall(m.keys, after.keys, 10) >= 0.95
+    # the rebuilt graph is as good as a fresh build over the live rows
+    fresh = vsg.Index(dim, metric, quant, 16, 128, 64, seed=3)
+    fresh.add(live, x[live])
+    r_fresh = recall(fresh.search(q, 10, 64).keys, after.keys, 10)
+    assert recall(m.keys, after.keys, 10) >= r_fresh - 0.02
     if metric == "l2sq":  # oracle over the live rows (integer data: exact distances)
         ok, od, _ = O.exact_search("l2sq", x[live], q, 10)
         np.testing.assert_array_equal(after.distances, od)
@@ -53,8 +57,9 @@ def test_compact_keeps_exact_answers_and_recall(metric, quant):
     # dropped keys can come back; compacted keys can go
     idx.add(dead[:100], x[dead[:100]])
     assert idx.remove(live[:10]) == 10
-    m = idx.search(x[dead[:100]], 1, 64)
-    assert (m.keys[:, 0] == dead[:100]).mean() > 0.95
+    if metric != "ip":  # self is the nearest neighbour under l2sq / cos
+        m = idx.search(x[dead[:100]], 1, 64)
+        assert (m.keys[:, 0] == dead[:100]).mean() > 0.95
 
 
 def test_compact_everything_and_exact_only():

@@ -122,3 +122,25 @@ def test_http_status_codes(server):
     assert client._req("GET", f"{client.url_api}/nope")[0] == 404
     st, body = client._req("GET", f"{client.url_api}/indexes/vector/ann/count")
     assert st == 200 and json.loads(body) == 0
+
+
+def test_http_burst_of_concurrent_clients(server):
+    """64 simultaneous connections (the listen backlog must not reset them)."""
+    import threading
+    srv, client = server
+    srv.engine.add_index(META)
+    idx = srv.engine.get_index(META.id)
+    for i in range(20):
+        idx.add_or_replace((i, str(i)), [i, 0, 0])
+    out = [None] * 256
+
+    def worker(t):
+        for i in range(t, 256, 64):
+            out[i] = client.ann(META, [i % 20, 0, 0], 1)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(64)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for i in range(256):
+        pks, dists = out[i]
+        assert pks["pk"] == [i % 20] and dists == [0.0]

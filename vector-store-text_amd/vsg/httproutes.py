@@ -204,13 +204,17 @@ def _handler(engine: Engine) -> Callable:
     return Handler
 
 
+class _Server(ThreadingHTTPServer):
+    request_queue_size = 1024  # listen backlog: the default 5 resets bursts of clients
+    daemon_threads = True
+
+
 class HttpServer:
     """src/httpserver.rs: the router served on a background thread."""
 
     def __init__(self, engine: Engine, addr: Tuple[str, int] = ("127.0.0.1", 0)):
         self.engine = engine
-        self._srv = ThreadingHTTPServer(addr, _handler(engine))
-        self._srv.daemon_threads = True
+        self._srv = _Server(addr, _handler(engine))
         self._thread = threading.Thread(target=self._srv.serve_forever, name="vsg-http", daemon=True)
         self._thread.start()
 

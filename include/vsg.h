@@ -202,7 +202,8 @@ int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t m
  * tokio/rayon tasks) with the GPU index behind it.  One worker thread per actor
  * drains the message FIFO and turns runs of single-vector adds and single-query
  * anns into batched GPU calls; capacity grows like
- * usearch.rs:200-212.  Messages apply in submission order (an ann sees every
+ * usearch.rs:200-212; tombstones left by removes and replaces are compacted
+ * away once they reach compact_percent of the stored rows.  Messages apply in submission order (an ann sees every
  * write submitted before it).  Every function is thread-safe; errors are
  * reported through vsg_last_error() like the index calls.  The PK<->u64
  * bimap stays in the caller, as in the reference (usearch.rs:109-113). */
@@ -214,6 +215,10 @@ typedef struct {
     uint64_t reserve_threshold; /* RESERVE_THRESHOLD (:67); 0 => increment / 3 */
     uint32_t max_batch;         /* messages drained per worker wake-up; 0 => 65536 */
     uint32_t max_wait_us;       /* optional coalescing window; 0 => natural batching */
+    uint32_t compact_percent;   /* vsg_index_compact once tombstones >= this % of stored
+                                   rows; 0 => 50, >= 100 => never */
+    uint32_t reserved;
+    uint64_t compact_min_dead;  /* ... and at least this many; 0 => 4096 */
 } vsg_actor_options_t;
 
 typedef struct {
@@ -221,6 +226,7 @@ typedef struct {
     uint64_t add_calls, remove_calls, search_calls, reserve_calls;
     uint64_t add_errors, remove_errors, search_errors;
     uint64_t max_search_batch, max_add_batch;
+    uint64_t compactions, compacted_rows, compact_errors;
 } vsg_actor_counters_t;
 
 /* replaces usearch::new (the actor spawn + Index::new + reserve(1M)) — usearch.rs:82-139 */

@@ -247,11 +247,79 @@ static void test_add_errors_swallowed() {
     CHECK(a.counters().add_errors == 1);
 }
 
+// 5) tombstones (removes, and the old row of every replace) trigger a
+//    compaction once they reach compact_percent of the stored rows
+struct TombMock final : vsg::ActorBackend {
+    std::map<uint64_t, int> live;
+    size_t stored = 0, cap = 0, compactions = 0;
+    size_t dimensions() const override { return 1; }
+    size_t size() const override { return live.size(); }
+    size_t capacity() const override { return cap; }
+    size_t expansion_search() const override { return 4; }
+    bool contains(uint64_t k) const override { return live.count(k) != 0; }
+    int reserve(size_t c) override {
+        cap = std::max(cap, c);
+        return 0;
+    }
+    int add(const uint64_t* k, const float*, size_t n) override {
+        for (size_t i = 0; i < n; ++i) live[k[i]] = 1;
+        stored += n;
+        return 0;
+    }
+    int remove(const uint64_t* k, size_t n, size_t* r) override {
+        size_t c = 0;
+        for (size_t i = 0; i < n; ++i) c += live.erase(k[i]);
+        if (r) *r = c;
+        return 0;
+    }
+    int search(const float*, size_t, size_t, size_t, uint64_t*, float*, size_t*) override { return 0; }
+    size_t slots() const override { return stored; }
+    int compact(size_t* dropped) override {
+        *dropped = stored - live.size();
+        stored = live.size();
+        ++compactions;
+        return 0;
+    }
+};
+
+static void test_auto_compaction() {
+    auto* m = new TombMock;
+    TombMock* mp = m;
+    vsg::ActorConfig cfg;
+    cfg.compact_percent = 50;
+    cfg.compact_min_dead = 100;
+    vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), cfg);
+    CHECK(a.init() == 0);
+    float v = 1.f;
+    for (uint64_t k = 0; k < 200; ++k) a.add_or_replace(k, &v);
+    CHECK(a.flush() == 0 && mp->compactions == 0);
+    for (uint64_t k = 0; k < 150; ++k) a.add_or_replace(k, &v);  // 150 replaces: 150 dead of 350
+    CHECK(a.flush() == 0 && mp->compactions == 0);
+    // 60 more: the ratio crosses 50 % after the 25th (200 dead of 400) or, with
+    // coarser batching, later; exactly one compaction either way
+    for (uint64_t k = 0; k < 60; ++k) a.add_or_replace(k, &v);
+    CHECK(a.flush() == 0 && mp->compactions == 1);
+    const size_t dropped = a.counters().compacted_rows;
+    CHECK(dropped >= 200 && dropped <= 210 && mp->stored == 200 + (210 - dropped));
+    for (uint64_t k = 0; k < 80; ++k) a.remove(k);  // <= 90 dead: under compact_min_dead
+    CHECK(a.flush() == 0 && mp->compactions == 1);
+    size_t n = 0;
+    CHECK(a.count(&n) == 0 && n == 120);
+    cfg.compact_percent = 100;  // disabled
+    auto* m2 = new TombMock;
+    vsg::Actor b(std::unique_ptr<vsg::ActorBackend>(m2), cfg);
+    CHECK(b.init() == 0);
+    for (int r = 0; r < 5; ++r)
+        for (uint64_t k = 0; k < 200; ++k) b.add_or_replace(k, &v);
+    CHECK(b.flush() == 0 && m2->compactions == 0 && m2->stored == 1000);
+}
+
 int main() {
     test_fifo_semantics();
     test_concurrent_anns();
     test_ef_groups_and_errors();
     test_add_errors_swallowed();
+    test_auto_compaction();
     std::printf("ok\n");
     return 0;
 }

@@ -49,6 +49,12 @@ struct ActorBackend {
     virtual int search(const float* q, size_t nq, size_t k, size_t ef, uint64_t* keys, float* dist,
                        size_t* counts) = 0;
     virtual const char* last_error() const { return ""; }
+    // stored rows including tombstones, and dropping the tombstones
+    virtual size_t slots() const { return size(); }
+    virtual int compact(size_t* dropped) {
+        if (dropped) *dropped = 0;
+        return 0;
+    }
 };
 
 struct ActorConfig {
@@ -56,6 +62,11 @@ struct ActorConfig {
     size_t reserve_threshold = 333333;   // RESERVE_THRESHOLD = increment / 3, :67
     size_t max_batch = 65536;            // messages drained per worker wake-up
     uint32_t max_wait_us = 0;            // optional coalescing window (0: natural batching)
+    // compact once tombstones reach this percentage of the stored rows (and at
+    // least compact_min_dead rows); >= 100 disables.  Replaces keep the old row
+    // as a tombstone (usearch.rs:214-221), so an upsert stream needs this.
+    uint32_t compact_percent = 50;
+    size_t compact_min_dead = 4096;
 };
 
 struct ActorCounters {
@@ -63,6 +74,7 @@ struct ActorCounters {
     uint64_t add_calls = 0, remove_calls = 0, search_calls = 0, reserve_calls = 0;
     uint64_t add_errors = 0, remove_errors = 0, search_errors = 0;
     uint64_t max_search_batch = 0, max_add_batch = 0;
+    uint64_t compactions = 0, compacted_rows = 0, compact_errors = 0;
 };
 
 class Actor {
@@ -226,6 +238,7 @@ class Actor {
             if (b[i].kind == ADD || b[i].kind == REMOVE) {
                 while (j < b.size() && (b[j].kind == ADD || b[j].kind == REMOVE)) ++j;
                 writes(b, i, j);
+                maybe_compact();
             } else if (b[i].kind == ANN) {
                 while (j < b.size() && b[j].kind == ANN) ++j;
                 anns(b, i, j);
@@ -306,6 +319,19 @@ class Actor {
             if (rc) ctr_.add_errors += s.add.size();
         }
         s.clear();
+    }
+
+    void maybe_compact() {
+        if (cfg_.compact_percent >= 100) return;
+        const size_t slots = be_->slots(), live = be_->size();
+        const size_t dead = slots > live ? slots - live : 0;
+        if (dead < cfg_.compact_min_dead || dead * 100 < (size_t)cfg_.compact_percent * slots) return;
+        size_t dropped = 0;
+        const int rc = be_->compact(&dropped);
+        std::lock_guard<std::mutex> lk(cm_);
+        ctr_.compactions++;
+        ctr_.compacted_rows += dropped;
+        if (rc) ctr_.compact_errors++;
     }
 
     // ------------------------------------------------------------------ anns --

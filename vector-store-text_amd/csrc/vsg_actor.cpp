@@ -34,6 +34,11 @@ struct IndexBackend final : vsg::ActorBackend {
                size_t* counts) override {
         return vsg_index_search(h, q, nq, k, e, keys, dist, counts);
     }
+    size_t slots() const override {
+        size_t s = 0;
+        return vsg_index_graph_info(h, &s, nullptr, nullptr, nullptr, nullptr) == VSG_OK ? s : size();
+    }
+    int compact(size_t* dropped) override { return vsg_index_compact(h, dropped); }
     // called on the worker thread, right after the failing call
     const char* last_error() const override { return vsg_last_error(); }
 };
@@ -58,6 +63,8 @@ int vsg_actor_new(const vsg_actor_options_t* o, vsg_actor_t** out) {
     cfg.reserve_threshold = o->reserve_threshold ? o->reserve_threshold : cfg.reserve_increment / 3;
     if (o->max_batch) cfg.max_batch = o->max_batch;
     cfg.max_wait_us = o->max_wait_us;
+    if (o->compact_percent) cfg.compact_percent = o->compact_percent;
+    if (o->compact_min_dead) cfg.compact_min_dead = o->compact_min_dead;
     const size_t ef = o->index.expansion_search ? o->index.expansion_search : 64;
     auto* a = new vsg_actor;
     a->index = h;
@@ -136,6 +143,9 @@ int vsg_actor_counters(const vsg_actor_t* a, vsg_actor_counters_t* out) {
     out->search_errors = c.search_errors;
     out->max_search_batch = c.max_search_batch;
     out->max_add_batch = c.max_add_batch;
+    out->compactions = c.compactions;
+    out->compacted_rows = c.compacted_rows;
+    out->compact_errors = c.compact_errors;
     return VSG_OK;
 }
 

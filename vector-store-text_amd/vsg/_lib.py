@@ -87,6 +87,9 @@ class ActorOptions(C.Structure):
         ("reserve_threshold", C.c_uint64),
         ("max_batch", C.c_uint32),
         ("max_wait_us", C.c_uint32),
+        ("compact_percent", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("compact_min_dead", C.c_uint64),
     ]
 
 
@@ -94,7 +97,7 @@ class ActorCounters(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in (
         "messages", "writes", "anns", "counts", "add_calls", "remove_calls", "search_calls",
         "reserve_calls", "add_errors", "remove_errors", "search_errors", "max_search_batch",
-        "max_add_batch")]
+        "max_add_batch", "compactions", "compacted_rows", "compact_errors")]
 
 
 _lib = None

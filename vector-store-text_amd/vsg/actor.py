@@ -27,11 +27,12 @@ class Actor:
     def __init__(self, dimensions: int, metric: str = "l2sq", quantization: str = "f32",
                  connectivity: int = 0, expansion_add: int = 0, expansion_search: int = 0,
                  device: int = 0, seed: int = 0, reserve_increment: int = 0, reserve_threshold: int = 0,
-                 max_batch: int = 0, max_wait_us: int = 0):
+                 max_batch: int = 0, max_wait_us: int = 0, compact_percent: int = 0, compact_min_dead: int = 0):
         self.dimensions = int(dimensions)
         opt = ActorOptions(Options(self.dimensions, METRICS[metric], SCALARS[quantization], connectivity,
                                    expansion_add, expansion_search, device, 0, seed),
-                           reserve_increment, reserve_threshold, max_batch, max_wait_us)
+                           reserve_increment, reserve_threshold, max_batch, max_wait_us, compact_percent, 0,
+                           compact_min_dead)
         h = C.c_void_p()
         check(lib().vsg_actor_new(C.byref(opt), C.byref(h)))
         self._h = h

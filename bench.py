@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--efc", type=int, default=128)
     ap.add_argument("--ef", type=int, default=0, help="fixed ef (0 = sweep for recall >= target)")
     ap.add_argument("--target-recall", type=float, default=0.95)
+    ap.add_argument("--config-ef", type=int, default=128,
+                    help="also time the config's nominal efSearch (BASELINE configs[1]: 128); 0 = skip")
     ap.add_argument("--config", type=int, default=1, help="seed set (BASELINE.json configs index)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
@@ -239,6 +241,23 @@ def hnsw_leg(c, mode):
     row_bytes = ((a.dim + per16 - 1) // per16) * 16
     alg_bytes = (st["search_distances"] * row_bytes + st["search_adjacency"] * 2 * a.M * 4) / a.steps
     kern_ms_avg = kern_ms / a.steps
+
+    # the config's nominal efSearch, timed the same way (reported beside the headline)
+    at_cfg = None
+    if a.config_ef and a.config_ef != ef:
+        e2 = a.config_ef
+        r2 = recall_of(search(qgt, e2, kshard(e2))[0])
+        for _ in range(max(1, a.warmup)):
+            search(q, e2, kshard(e2))
+        c.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            search(q, e2, kshard(e2))
+            torch.cuda.synchronize()
+        c.barrier()
+        el2 = c.max_over_ranks(time.perf_counter() - t0)
+        at_cfg = {"ef": e2, "k_shard": kshard(e2), "qps": round(queries_done / el2, 1),
+                  "ms_per_step": round(1000.0 * el2 / a.steps, 3), "recall_at_10": round(r2, 4)}
     return {
         "mode": mode, "index": index, "q": q, "x": x, "nloc": nloc,
         "qps": queries_done / elapsed, "ms_per_step": 1000.0 * elapsed / a.steps,
@@ -249,6 +268,7 @@ def hnsw_leg(c, mode):
         "dist_per_query": st["search_distances"] / max(1, st["search_queries"]),
         "build_dist_per_vector": bstats["build_distances"] / max(1, nloc),
         "build_batches": bstats["build_batches"],
+        "at_config_ef": at_cfg,
     }
 
 
@@ -312,6 +332,7 @@ def main():
                      "dist_evals_per_query": round(head["dist_per_query"], 1)},
         "build_stats": {"distance_evals_per_vector": round(head["build_dist_per_vector"], 1),
                         "batches": head["build_batches"]},
+        "at_config_ef": head["at_config_ef"],
     }
     if "shard" in res and head["mode"] != "shard":
         s = res["shard"]
@@ -321,7 +342,8 @@ def main():
                              "build_seconds": round(s["build_s"], 3),
                              "kernel_ms": round(s["kern_ms"], 3),
                              "dist_evals_per_query_per_shard": round(s["dist_per_query"], 1),
-                             "scaling": "strong", "note": "row-range shards, every query searched on every shard"}
+                             "scaling": "strong", "note": "row-range shards, every query searched on every shard",
+                             "at_config_ef": s["at_config_ef"]}
     # CPU baseline (rank 0, N=1 only): oracle/ restatement of usearch
     if world == 1 and rank == 0 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(a, head["index"], head["q"], head["ef"], head["x"])

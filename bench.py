@@ -150,6 +150,9 @@ def hnsw_leg(c, mode):
         keys_np = keys_np[order]
     torch.cuda.synchronize()
 
+    per16 = 4 if a.quant == "f32" else 8
+    row_bytes = ((a.dim + per16 - 1) // per16) * 16
+
     # build (timed; not part of the QPS step)
     seed = 0x5EED + (rank if sharded else 0)
     index = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 128, device=c.local, seed=seed)
@@ -237,8 +240,6 @@ def hnsw_leg(c, mode):
     elapsed = c.max_over_ranks(time.perf_counter() - t0)
     queries_done = (world if replica else 1) * a.queries * a.steps
     st = index.stats()
-    per16 = 4 if a.quant == "f32" else 8
-    row_bytes = ((a.dim + per16 - 1) // per16) * 16
     alg_bytes = (st["search_distances"] * row_bytes + st["search_adjacency"] * 2 * a.M * 4) / a.steps
     kern_ms_avg = kern_ms / a.steps
 
@@ -267,6 +268,9 @@ def hnsw_leg(c, mode):
         "achieved_gbs": alg_bytes / (kern_ms_avg * 1e-3) / 1e9,
         "dist_per_query": st["search_distances"] / max(1, st["search_queries"]),
         "build_dist_per_vector": bstats["build_distances"] / max(1, nloc),
+        # algorithmic bytes of the whole build: every distance evaluation reads one
+        # row, every adjacency visit one 2M-entry level-0 row (upper rows are shorter)
+        "build_alg_bytes": bstats["build_distances"] * row_bytes + bstats["build_adjacency"] * 2 * a.M * 4,
         "build_batches": bstats["build_batches"],
         "at_config_ef": at_cfg,
     }
@@ -332,6 +336,12 @@ def main():
                      "dist_evals_per_query": round(head["dist_per_query"], 1)},
         "build_stats": {"distance_evals_per_vector": round(head["build_dist_per_vector"], 1),
                         "batches": head["build_batches"]},
+        # whole-build wall time (insert + sort + reverse-link launches and host gaps)
+        "build_roofline": {"bound": "hbm",
+                           "achieved": round(head["build_alg_bytes"] / head["build_s"] / 1e9, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(head["build_alg_bytes"] / head["build_s"] / 1e9 / HBM_PEAK_GBS, 4),
+                           "alg_bytes": int(head["build_alg_bytes"])},
         "at_config_ef": head["at_config_ef"],
     }
     if "shard" in res and head["mode"] != "shard":

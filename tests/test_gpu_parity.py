@@ -434,3 +434,40 @@ def test_search_batch_invariance(dim, metric):
             np.testing.assert_array_equal(m.keys, full.keys[s:s + bsz], err_msg=f"batch {bsz} at {s}")
             np.testing.assert_array_equal(m.distances, full.distances[s:s + bsz])
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("waves", ["2", "4"])
+def test_hnsw_cooperative_search_bitexact(waves, monkeypatch):
+    """Cooperative large-ef kernel (several waves share one query's visited
+    table and list): bit-exact vs the oracle on integer data, including a
+    forgetful visited table (duplicates re-evaluated and de-duplicated), and
+    identical to the single-wave kernel on float data."""
+    n, dim = 6000, 64
+    x = G.uint8_valued(n, dim, 51).astype(np.float32)
+    q = G.uint8_valued(80, dim, 52).astype(np.float32)
+    h = O.HnswOracle(dim, "l2sq", 16, 64, 48, seed=7)
+    h.add(np.arange(n), x)
+    h.remove(np.arange(0, n, 23))
+    idx = vsg.Index(dim, "l2sq", connectivity=16, expansion_add=64, expansion_search=48, seed=7)
+    idx.import_graph(h.export())
+    monkeypatch.setenv("VSG_SEARCH_WAVES", waves)
+    for ef, factor in ((10, "6"), (128, "6"), (400, "1"), (1024, "12")):
+        monkeypatch.setenv("VSG_SEARCH_HASH_FACTOR", factor)
+        ok, od, oc = h.search(q, 10, ef)
+        m = idx.search(q, 10, ef)
+        np.testing.assert_array_equal(m.counts, oc)
+        np.testing.assert_array_equal(m.keys, ok)
+        np.testing.assert_array_equal(m.distances, od)
+    # float data, cosine, GPU-built graph: cooperative == single-wave
+    xf = G.clustered(8000, 96, 53, 9)
+    qf = G.clustered(200, 96, 54, 9)
+    b = vsg.Index(96, "cos", connectivity=16, expansion_add=64, expansion_search=64, seed=2)
+    b.add(np.arange(len(xf)), xf)
+    monkeypatch.delenv("VSG_SEARCH_HASH_FACTOR")
+    for ef in (64, 300):
+        monkeypatch.setenv("VSG_SEARCH_WAVES", "1")
+        a1 = b.search(qf, 10, ef)
+        monkeypatch.setenv("VSG_SEARCH_WAVES", waves)
+        a2 = b.search(qf, 10, ef)
+        np.testing.assert_array_equal(a1.keys, a2.keys)
+        np.testing.assert_array_equal(a1.distances, a2.distances)

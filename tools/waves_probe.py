@@ -1,0 +1,60 @@
+"""Search QPS vs waves per query (VSG_SEARCH_WAVES), one build.
+
+usage (GPU box): python tools/waves_probe.py rows dim metric quant data efs waves
+  efs, waves: comma lists, e.g. 36,128,321 1,2,4
+prints one JSON line per (ef, waves): QPS over 10,000 queries, recall@10 (200
+queries vs exact) and whether keys/distances equal the 1-wave kernel's.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "vector-store-text_amd"))
+
+
+def main():
+    rows, dim, metric, quant, data = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+    efs = [int(e) for e in sys.argv[6].split(",")]
+    waves = [int(w) for w in sys.argv[7].split(",")]
+    import torch
+    import vsg
+
+    from vsg import datagen as G
+
+    bs, qs, ms = G.config_seeds(3 if data == "sift" else 2)
+    x = vsg.datagen_device(data, rows, dim, bs, ms)
+    q = vsg.datagen_device(data, 10000, dim, qs, ms)
+    idx = vsg.Index(dim, metric, quant, 16, 128, 64, seed=1)
+    t0 = time.time()
+    idx.add_device(np.arange(rows, dtype=np.uint64), x)
+    torch.cuda.synchronize()
+    bt = time.time() - t0
+    del x
+    gt = idx.search_device(q[:200], 10, exact=True)[0].cpu().numpy()
+    for ef in efs:
+        base = None
+        for w in waves:
+            os.environ["VSG_SEARCH_WAVES"] = str(w)
+            kk, dd = idx.search_device(q, 10, ef)[:2]
+            kk, dd = kk.cpu().numpy(), dd.cpu().numpy()
+            if base is None:
+                base = (kk, dd)
+            same = bool((kk == base[0]).all() and (dd == base[1]).all())
+            rec = float(np.mean([len(set(a) & set(b)) / 10 for a, b in zip(kk[:200], gt)]))
+            torch.cuda.synchronize()
+            t0 = time.time()
+            for _ in range(3):
+                idx.search_device(q, 10, ef)
+            torch.cuda.synchronize()
+            dt = (time.time() - t0) / 3
+            print(json.dumps({"rows": rows, "dim": dim, "metric": metric, "quant": quant, "ef": ef, "waves": w,
+                              "build_s": round(bt, 2), "qps": round(10000 / dt, 1), "recall": round(rec, 4),
+                              "same_as_1wave": same}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -32,11 +32,14 @@ __host__ __device__ int hash_size_for(int ef, int factor) {
     return (int)h;
 }
 
-static size_t wave_lds_bytes(int hash, int cap, bool with_sel) {
+static __host__ __device__ size_t wave_lds_bytes(int hash, int cap, bool with_sel) {
     return (size_t)hash * 4 + (size_t)cap * 16 + 64 * 4 * 4 + (with_sel ? 64 * 4 * 2 : 0);
 }
 
-size_t search_lds_bytes(int ef, int hash) { return wave_lds_bytes(hash, ef, false); }
+// cooperative search: + 8 control words (WgCtl) after the shared wave state
+size_t search_lds_bytes(int ef, int hash, int waves) {
+    return wave_lds_bytes(hash, ef, false) + (waves > 1 ? 32 : 0);
+}
 size_t insert_lds_bytes(int efc, int hash) { return wave_lds_bytes(hash, efc, true); }
 
 static __device__ inline GraphDev to_dev(const DevGraph& g) {
@@ -288,6 +291,163 @@ __global__ __launch_bounds__(64) void hnsw_search_kernel(SearchParams p) {
     }
 }
 
+// ------------------------------------------------------ search: cooperative --
+// Large ef: NW waves share ONE query's LDS state (visited hash, list).  Per
+// expansion: wave 0 picks the best unexpanded entry, reads its adjacency row and
+// records fresh neighbours (serial control, as in beam_level); the fresh rows'
+// distances are split over the NW waves (NW x the loads in flight per LDS byte,
+// 1/NW of the latency); wave 0 ranks the candidates (List::place) and every
+// thread moves the existing entries (List::shift).  Same expansion order and
+// same list as hnsw_search_kernel, hence the same results (tested bit-exact
+// against the oracle).  Upper levels: wave 0 alone (greedy_level).
+//
+// Control words in LDS (ctl[8]): [0..3] (done, cnt) double-buffered by
+// iteration parity (a wave still reading iteration i's words never sees i+1's:
+// wave 0 cannot reach i+2 without the barrier that wave joins after reading),
+// [4..5] nc by parity, [6..7] level-0 entry (slot, distance bits).
+
+template <int G, int VM, int U, typename T, int MET, int NW>
+__device__ void beam0_wg(const GraphDev& g, const QReg<G, VM, T>& q, WaveLds& w, int* ctl, uint64_t& ndist,
+                         uint64_t& nadj) {
+    constexpr int NT = 64 * NW;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = lane_id();
+    const int m = g.M0;
+    List& L = w.list;
+    L.cur = 0;
+    L.size = 1;
+    {
+        uint4* t4 = reinterpret_cast<uint4*>(w.vis.tab);
+        for (uint32_t i = tid; i < w.vis.size / 4; i += NT)
+            t4[i] = make_uint4(VSG_EMPTY, VSG_EMPTY, VSG_EMPTY, VSG_EMPTY);
+    }
+    __syncthreads();
+    bool lossy = false;  // wave 0 only
+    if (tid == 0) {
+        const uint32_t ep = (uint32_t)ctl[6];
+        bool unrec;
+        w.vis.insert(ep, unrec);
+        L.d0[0] = __int_as_float(ctl[7]);
+        L.i0[0] = ep;
+    }
+    __syncthreads();
+    for (int it = 0;; ++it) {
+        int* c2 = ctl + 2 * (it & 1);
+        if (wave == 0) {
+            const int p = L.first_unexpanded();
+            int cnt = 0;
+            if (p >= 0) {
+                const uint32_t node = L.I()[p] & VSG_ID_MASK;
+                wave_sync();
+                if (lane == 0) L.I()[p] = node | VSG_EXP_BIT;
+                const uint32_t* row = g.row(node, 0);
+                const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
+                ++nadj;
+                bool fresh = false, evicted = false;
+                if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
+                const uint64_t mask = __ballot(fresh);
+                lossy = lossy || __ballot(evicted) != 0;
+                cnt = popc64(mask);
+                if (fresh) w.todo[lanes_below(mask)] = nb;
+            }
+            if (lane == 0) {
+                c2[0] = p < 0;
+                c2[1] = cnt;
+            }
+        }
+        __syncthreads();
+        if (c2[0]) break;
+        const int cnt = c2[1];
+        if (cnt == 0) continue;  // parity double-buffering makes the next write safe
+        const int per = (cnt + NW - 1) / NW;
+        const int b0 = wave * per;
+        const int c = min(cnt - b0, per);
+        if (c > 0) rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo + b0, c, q, w.tdist + b0);
+        __syncthreads();
+        if (wave == 0) {
+            ndist += (uint64_t)cnt;
+            const bool valid = lane < cnt;
+            const float cd = valid ? w.tdist[lane] : 0.f;
+            const uint32_t ci = valid ? w.todo[lane] : 0u;
+            const int nc = L.place(valid, cd, ci, lossy, w.sd, w.si);
+            if (lane == 0) ctl[4 + (it & 1)] = nc;
+        }
+        __syncthreads();
+        const int nc = ctl[4 + (it & 1)];
+        if (nc) L.shift(nc, w.sd, w.si, tid, NT);
+        L.advance(nc);
+        __syncthreads();
+    }
+}
+
+template <int G, int VM, int U, typename T, int MET, int NW>
+__global__ __launch_bounds__(64 * NW) void hnsw_search_wg_kernel(SearchParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    int qi = blockIdx.x;
+    if (p.xcd_map) {
+        const int nq = p.nq, qd = nq >> 3, rm = nq & 7;
+        const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+        qi = x * qd + min(x, rm) + j;
+    }
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = lane_id();
+    const GraphDev g = to_dev(p.g);
+    WaveLds w = carve(smem, p.ef, p.hash_size, false);
+    int* ctl = reinterpret_cast<int*>(smem + wave_lds_bytes(p.hash_size, p.ef, false));
+    uint64_t ndist = 0, nadj = 0;
+    int count = 0;
+    uint64_t* ok = p.out_keys + (size_t)qi * p.k;
+    float* od = p.out_dist + (size_t)qi * p.k;
+    if (p.entry != VSG_EMPTY) {
+        QReg<G, VM, T> q;
+        q.load(p.queries + (size_t)qi * g.row_bytes, g.nchunks);
+        if (wave == 0) {
+            uint32_t cur = p.entry;
+            float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
+            ++ndist;
+            for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+            if (lane == 0) {
+                ctl[6] = (int)cur;
+                ctl[7] = __float_as_int(dcur);
+            }
+        }
+        __syncthreads();
+        beam0_wg<G, VM, U, T, MET, NW>(g, q, w, ctl, ndist, nadj);
+        if (wave == 0) {
+            const List& L = w.list;
+            for (int r = 0; r < L.size && count < p.k; r += 64) {
+                const int i = r + lane;
+                const bool valid = i < L.size;
+                const uint32_t id = valid ? (L.I()[i] & VSG_ID_MASK) : 0u;
+                const bool alive = valid && !(p.flags[id] & 1);
+                const uint64_t m = __ballot(alive);
+                const int pos = count + lanes_below(m);
+                if (alive && pos < p.k) {
+                    ok[pos] = p.keys[id];
+                    od[pos] = L.D()[i];
+                }
+                count += popc64(m);
+            }
+            if (count > p.k) count = p.k;
+        }
+    }
+    if (wave != 0) return;
+    for (int j = count + lane; j < p.k; j += 64) {
+        ok[j] = ~0ull;
+        od[j] = __builtin_inff();
+    }
+    if (lane == 0) {
+        if (p.out_counts) p.out_counts[qi] = (uint32_t)count;
+        if (p.stats) {
+            atomicAdd(&p.stats[0], (unsigned long long)ndist);
+            atomicAdd(&p.stats[1], (unsigned long long)nadj);
+            atomicAdd(&p.stats[2], 1ull);
+        }
+    }
+}
+
 // ------------------------------------------------------------ build: fwd --
 // One wave per new node of the batch: descend, beam with efC per level,
 // select M_l neighbours, write the node's own rows and emit (level, v, u)
@@ -443,23 +603,32 @@ bool shape_supported(int nchunks) { return nchunks >= 1 && nchunks <= 1024; }
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s) {
     if (p.nq <= 0) return hipSuccess;
-    const size_t lds = search_lds_bytes(p.ef, p.hash_size);
+    const int nw = p.waves == 2 || p.waves == 4 ? p.waves : 1;
+    const size_t lds = search_lds_bytes(p.ef, p.hash_size, nw);
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
-        auto kern = VSG_KERNEL_OF(hnsw_search_kernel, sh, tt, mt);
-        if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        // <= 4M queries per dispatch (64 work-items each: the AQL grid size is 32-bit)
-        constexpr int CH = 1 << 22;
-        for (int off = 0; off < p.nq && err == hipSuccess; off += CH) {
-            SearchParams c = p;
-            c.nq = min(CH, p.nq - off);
-            c.queries = p.queries + (size_t)off * p.g.row_bytes;
-            c.out_keys = p.out_keys + (size_t)off * p.k;
-            c.out_dist = p.out_dist + (size_t)off * p.k;
-            c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
-            hipLaunchKernelGGL(kern, dim3(c.nq), dim3(64), lds, s, c);
-            err = hipGetLastError();
-        }
+        auto run = [&](auto kern) {
+            if (lds > 65536)
+                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            // <= 1M queries per dispatch (<= 256 work-items each: the AQL grid size is 32-bit)
+            constexpr int CH = 1 << 20;
+            for (int off = 0; off < p.nq && err == hipSuccess; off += CH) {
+                SearchParams c = p;
+                c.nq = min(CH, p.nq - off);
+                c.queries = p.queries + (size_t)off * p.g.row_bytes;
+                c.out_keys = p.out_keys + (size_t)off * p.k;
+                c.out_dist = p.out_dist + (size_t)off * p.k;
+                c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
+                hipLaunchKernelGGL(kern, dim3(c.nq), dim3(64 * nw), lds, s, c);
+                err = hipGetLastError();
+            }
+        };
+        constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
+        using T = typename decltype(tt)::T;
+        constexpr int MET = decltype(mt)::MET;
+        if (nw == 1) run(hnsw_search_kernel<G, VM, U, T, MET>);
+        else if (nw == 2) run(hnsw_search_wg_kernel<G, VM, U, T, MET, 2>);
+        else run(hnsw_search_wg_kernel<G, VM, U, T, MET, 4>);
     });
     return err;
 }

@@ -295,6 +295,70 @@ struct List {
         cur ^= 1;
         wave_sync();
     }
+
+    // merge() split for a multi-wave workgroup sharing this list (every wave
+    // holds an identical copy of cur / size).  place(): ONE wave filters and
+    // ranks its candidates, writes them sorted to sd/si and into the next
+    // buffer, and returns nc (wave-uniform).  After a workgroup barrier, every
+    // thread of the group calls shift() (existing entries -> next buffer), then
+    // advance(nc) and another barrier.  Same result as merge().
+    __device__ int place(bool valid, float cd, uint32_t ci, bool maybe_dup, float* sd, uint32_t* si) const {
+        if (valid && size == cap) {
+            const float wd = D()[size - 1];
+            const uint32_t wi = I()[size - 1] & VSG_ID_MASK;
+            valid = cand_less(cd, ci, wd, wi);
+        }
+        if (valid && maybe_dup) {
+            const int p = lower_bound(cd, ci);
+            if (p < size && D()[p] == cd && (I()[p] & VSG_ID_MASK) == ci) valid = false;
+        }
+        const uint64_t mask = __ballot(valid);
+        const int nc = popc64(mask);
+        if (nc == 0) return 0;
+        int rank = 0;
+        for (uint64_t m = mask; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            rank += cand_less(readlane(cd, j), readlane(ci, j), cd, ci) ? 1 : 0;
+        }
+        if (valid) {
+            sd[rank] = cd;
+            si[rank] = ci;
+            const int pos_new = rank + lower_bound(cd, ci);
+            if (pos_new < cap) {
+                Dn()[pos_new] = cd;
+                In()[pos_new] = ci;
+            }
+        }
+        return nc;
+    }
+
+    __device__ void shift(int nc, const float* sd, const uint32_t* si, int tid, int nthreads) const {
+        const float* dd = D();
+        const uint32_t* ii = I();
+        float* nd = Dn();
+        uint32_t* ni = In();
+        for (int e = tid; e < size; e += nthreads) {
+            const float ed = dd[e];
+            const uint32_t ei = ii[e];
+            int lo = 0, hi = nc;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (cand_less(sd[mid], si[mid], ed, ei & VSG_ID_MASK)) lo = mid + 1;
+                else hi = mid;
+            }
+            const int p = e + lo;
+            if (p < cap) {
+                nd[p] = ed;
+                ni[p] = ei;
+            }
+        }
+    }
+
+    __device__ __forceinline__ void advance(int nc) {
+        if (nc == 0) return;
+        size = min(size + nc, cap);
+        cur ^= 1;
+    }
 };
 
 // ----------------------------------------------------------- graph access --

@@ -801,6 +801,10 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
             const int factor = (int)env_double("VSG_SEARCH_HASH_FACTOR", wide ? 12 : 6);
             p.hash_size = std::max(hash_size_for(p.ef, factor), wide ? 2048 : 1024);
         }
+        // waves per query: 1 = hnsw_search_kernel; 2 / 4 = cooperative kernel
+        // (large ef, where one wave is latency-bound on the list).  Same results;
+        // measured +5-7% at ef >= 321 (profiles/r01_search_waves.jsonl).
+        p.waves = (int)env_double("VSG_SEARCH_WAVES", p.ef >= 256 ? 2 : 1);
         err = launch_search(h->st, h->mk, p, s);
     } else if (err == hipSuccess) {
         ExactParams ep{};

@@ -33,6 +33,7 @@ struct SearchParams {
     unsigned long long* stats;  // [0] n_dist, [1] n_adj, [2] queries
     int xcd_map;                // 1: workgroups b, b+8, ... (one XCD) take consecutive queries
     int hash_size;              // visited-table entries (hash_size_for)
+    int waves;                  // waves per query: 1 (hnsw_search_kernel), 2 or 4 (cooperative)
 };
 
 struct InsertParams {
@@ -110,7 +111,7 @@ constexpr uint32_t MAX_SLOTS = 1u << 29;
 
 bool shape_supported(int nchunks);
 __host__ __device__ int hash_size_for(int ef, int factor);
-size_t search_lds_bytes(int ef, int hash);
+size_t search_lds_bytes(int ef, int hash, int waves = 1);
 size_t insert_lds_bytes(int efc, int hash);
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);

@@ -5,6 +5,7 @@ usage (GPU box): python tools/waves_probe.py rows dim metric quant data efs wave
 prints one JSON line per (ef, waves): QPS over 10,000 queries, recall@10 (200
 queries vs exact) and whether keys/distances equal the 1-wave kernel's.
 """
+import ctypes as C
 import json
 import os
 import sys
@@ -46,14 +47,23 @@ def main():
             same = bool((kk == base[0]).all() and (dd == base[1]).all())
             rec = float(np.mean([len(set(a) & set(b)) / 10 for a, b in zip(kk[:200], gt)]))
             torch.cuda.synchronize()
+            idx.reset_stats()
             t0 = time.time()
             for _ in range(3):
                 idx.search_device(q, 10, ef)
             torch.cuda.synchronize()
             dt = (time.time() - t0) / 3
+            st = idx.stats()
+            raw = (C.c_uint64 * 16)()
+            vsg.lib().vsg_debug_counters(idx._h, raw)
+            nq = max(1, st["search_queries"])
+            extra = {"dist_per_query": round(st["search_distances"] / nq, 1),
+                     "expansions_per_query": round(st["search_adjacency"] / nq, 1)}
+            if raw[10] or raw[11]:  # profiling build: wave-microseconds per query per phase
+                extra.update({f"us_{k}": round(raw[i] / 100.0 / nq, 2) for k, i in (("adj", 10), ("dist", 11), ("merge", 12))})
             print(json.dumps({"rows": rows, "dim": dim, "metric": metric, "quant": quant, "ef": ef, "waves": w,
                               "build_s": round(bt, 2), "qps": round(10000 / dt, 1), "recall": round(rec, 4),
-                              "same_as_1wave": same}), flush=True)
+                              "same_as_1wave": same, **extra}), flush=True)
 
 
 if __name__ == "__main__":

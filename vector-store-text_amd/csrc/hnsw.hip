@@ -148,10 +148,25 @@ __device__ void greedy_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, 
     }
 }
 
+// Search-phase clocks (100 MHz wall clock), summed per wave into stats[10..13]
+// when built with -DVSG_SEARCH_PROFILE (tools only; zero cost otherwise).
+struct BeamProf {
+    uint64_t adj = 0, dist = 0, merge = 0;
+};
+#ifdef VSG_SEARCH_PROFILE
+#define VSG_CLK() wall_clock64()
+#else
+#define VSG_CLK() 0ull
+#endif
+
 // usearch search_to_find_in_base_ restated (oracle beam()).
+// `hint`: entries below it are all expanded, so the scan for the next
+// candidate starts there (merge() reports the lowest position it filled).
+// (Prefetching the next entry's adjacency row during this expansion's distance
+// loads measured 2-7% slower: profiles/r01_search_phases.jsonl.)
 template <int G, int VM, int U, typename T, int MET>
 __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t ep, float dep,
-                           WaveLds& w, uint64_t& ndist, uint64_t& nadj) {
+                           WaveLds& w, uint64_t& ndist, uint64_t& nadj, BeamProf& pf) {
     const int lane = lane_id();
     const int m = l == 0 ? g.M0 : g.M;
     w.vis.clear();
@@ -166,12 +181,15 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
         L.i0[0] = ep;
     }
     wave_sync();
+    int hint = 0;
     for (;;) {
-        const int p = L.first_unexpanded();
+        const uint64_t t0 = VSG_CLK();
+        const int p = L.first_unexpanded(hint);
         if (p < 0) break;
         const uint32_t node = L.I()[p] & VSG_ID_MASK;
         wave_sync();
         if (lane == 0) L.I()[p] = node | VSG_EXP_BIT;
+        hint = p + 1;
         const uint32_t* row = g.row(node, l);
         const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
         ++nadj;
@@ -182,6 +200,8 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
         const int cnt = popc64(mask);
         if (fresh) w.todo[lanes_below(mask)] = nb;
         wave_sync();
+        const uint64_t t1 = VSG_CLK();
+        pf.adj += t1 - t0;
         if (cnt == 0) continue;
         rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
         wave_sync();
@@ -190,7 +210,10 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
         const float cd = valid ? w.tdist[lane] : 0.f;
         const uint32_t ci = valid ? w.todo[lane] : 0u;
         wave_sync();
-        L.merge(valid, cd, ci, lossy, w.sd, w.si);
+        const uint64_t t2 = VSG_CLK();
+        pf.dist += t2 - t1;
+        hint = min(hint, L.merge(valid, cd, ci, lossy, w.sd, w.si));
+        pf.merge += VSG_CLK() - t2;
     }
 }
 
@@ -250,6 +273,7 @@ __global__ __launch_bounds__(64) void hnsw_search_kernel(SearchParams p) {
     const GraphDev g = to_dev(p.g);
     WaveLds w = carve(smem, p.ef, p.hash_size, false);
     uint64_t ndist = 0, nadj = 0;
+    BeamProf pf;
     int count = 0;
     uint64_t* ok = p.out_keys + (size_t)qi * p.k;
     float* od = p.out_dist + (size_t)qi * p.k;
@@ -260,7 +284,7 @@ __global__ __launch_bounds__(64) void hnsw_search_kernel(SearchParams p) {
         float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
         ++ndist;
         for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
-        beam_level<G, VM, U, T, MET>(g, q, 0, cur, dcur, w, ndist, nadj);
+        beam_level<G, VM, U, T, MET>(g, q, 0, cur, dcur, w, ndist, nadj, pf);
         const List& L = w.list;
         for (int r = 0; r < L.size && count < p.k; r += 64) {
             const int i = r + lane;
@@ -287,6 +311,11 @@ __global__ __launch_bounds__(64) void hnsw_search_kernel(SearchParams p) {
             atomicAdd(&p.stats[0], (unsigned long long)ndist);
             atomicAdd(&p.stats[1], (unsigned long long)nadj);
             atomicAdd(&p.stats[2], 1ull);
+#ifdef VSG_SEARCH_PROFILE
+            atomicAdd(&p.stats[10], (unsigned long long)pf.adj);
+            atomicAdd(&p.stats[11], (unsigned long long)pf.dist);
+            atomicAdd(&p.stats[12], (unsigned long long)pf.merge);
+#endif
         }
     }
 }
@@ -397,6 +426,7 @@ __global__ __launch_bounds__(64 * NW) void hnsw_search_wg_kernel(SearchParams p)
     WaveLds w = carve(smem, p.ef, p.hash_size, false);
     int* ctl = reinterpret_cast<int*>(smem + wave_lds_bytes(p.hash_size, p.ef, false));
     uint64_t ndist = 0, nadj = 0;
+    [[maybe_unused]] BeamProf pf;
     int count = 0;
     uint64_t* ok = p.out_keys + (size_t)qi * p.k;
     float* od = p.out_dist + (size_t)qi * p.k;
@@ -444,6 +474,11 @@ __global__ __launch_bounds__(64 * NW) void hnsw_search_wg_kernel(SearchParams p)
             atomicAdd(&p.stats[0], (unsigned long long)ndist);
             atomicAdd(&p.stats[1], (unsigned long long)nadj);
             atomicAdd(&p.stats[2], 1ull);
+#ifdef VSG_SEARCH_PROFILE
+            atomicAdd(&p.stats[10], (unsigned long long)pf.adj);
+            atomicAdd(&p.stats[11], (unsigned long long)pf.dist);
+            atomicAdd(&p.stats[12], (unsigned long long)pf.merge);
+#endif
         }
     }
 }
@@ -464,6 +499,7 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     const uint32_t node = p.nodes[bi];
     const int L = p.levels[bi];
     uint64_t ndist = 0, nadj = 0, nsel_d = 0;
+    BeamProf pf;
     QReg<G, VM, T> q;
     q.load(g.vec(node), g.nchunks);
     uint32_t cur = p.entry;
@@ -472,7 +508,7 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     for (int l = p.max_level; l > L; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
     uint32_t pos = p.pair_off[bi];
     for (int l = min(L, p.max_level); l >= 0; --l) {
-        beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+        beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, pf);
         const int m = l == 0 ? g.M0 : g.M;
         const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, m, nsel_d);
         uint32_t* row = g.row(node, l);

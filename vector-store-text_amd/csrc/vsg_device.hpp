@@ -211,10 +211,11 @@ struct List {
     __device__ __forceinline__ float* Dn() const { return cur ? d0 : d1; }
     __device__ __forceinline__ uint32_t* In() const { return cur ? i0 : i1; }
 
-    // first entry not yet expanded, or -1
-    __device__ __forceinline__ int first_unexpanded() const {
+    // first entry not yet expanded, or -1 (entries below `start` are known to
+    // be expanded)
+    __device__ __forceinline__ int first_unexpanded(int start = 0) const {
         const int lane = lane_id();
-        for (int r = 0; r < size; r += 64) {
+        for (int r = start; r < size; r += 64) {
             const int i = r + lane;
             const bool un = i < size && !(I()[i] & VSG_EXP_BIT);
             const uint64_t m = __ballot(un);
@@ -238,8 +239,9 @@ struct List {
 
     // Merge one candidate per lane (valid lanes only).  Candidates must have
     // distinct ids that are not in the list unless `maybe_dup` is set for them.
-    // sd/si: 64-entry LDS scratch.
-    __device__ void merge(bool valid, float cd, uint32_t ci, bool maybe_dup, float* sd, uint32_t* si) {
+    // sd/si: 64-entry LDS scratch.  Returns the lowest position a candidate
+    // took (entries below it are unchanged), or INT_MAX if none was placed.
+    __device__ int merge(bool valid, float cd, uint32_t ci, bool maybe_dup, float* sd, uint32_t* si) {
         const int lane = lane_id();
         if (valid && size == cap) {
             const float wd = D()[size - 1];
@@ -252,7 +254,7 @@ struct List {
         }
         const uint64_t mask = __ballot(valid);
         const int nc = popc64(mask);
-        if (nc == 0) return;
+        if (nc == 0) return 0x7fffffff;
         // rank among candidates
         int rank = 0;
         for (uint64_t m = mask; m; m &= m - 1) {
@@ -266,6 +268,7 @@ struct List {
             si[rank] = ci;
         }
         const int pos_new = valid ? rank + lower_bound(cd, ci) : 0;
+        const int first = readlane(pos_new, __builtin_ctzll(__ballot(valid && rank == 0)));
         wave_sync();
         float* dd = D();
         uint32_t* ii = I();
@@ -294,6 +297,7 @@ struct List {
         size = min(size + nc, cap);
         cur ^= 1;
         wave_sync();
+        return first;
     }
 
     // merge() split for a multi-wave workgroup sharing this list (every wave

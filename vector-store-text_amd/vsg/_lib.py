@@ -12,7 +12,7 @@ import re
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libvsg.so")
+LIB_PATH = os.environ.get("VSG_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libvsg.so")
 HEADER = os.path.join(REPO_ROOT, "include", "vsg.h")
 
 VSG_OK = 0

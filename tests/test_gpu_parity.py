@@ -184,10 +184,13 @@ def test_reference_integration_kat(metric):
 
 # ------------------------------------------------------------------- HNSW --
 
+@pytest.mark.parametrize("reg", ["1", "0"])
 @pytest.mark.parametrize("metric,dim,M", [("l2sq", 32, 8), ("l2sq", 128, 16), ("ip", 64, 16)])
-def test_hnsw_search_same_graph_bitexact(metric, dim, M):
+def test_hnsw_search_same_graph_bitexact(metric, dim, M, reg, monkeypatch):
     """Oracle-built graph imported into HBM: GPU traversal == oracle traversal
-    (integer data => exact distances => identical visiting order)."""
+    (integer data => exact distances => identical visiting order), for the
+    register-set kernel (default) and the LDS-list kernel."""
+    monkeypatch.setenv("VSG_SEARCH_REG", reg)
     n = 6000
     x = G.uint8_valued(n, dim, 31) / (16.0 if metric == "ip" else 1.0)
     q = G.uint8_valued(100, dim, 32) / (16.0 if metric == "ip" else 1.0)
@@ -450,6 +453,7 @@ def test_hnsw_cooperative_search_bitexact(waves, monkeypatch):
     h.remove(np.arange(0, n, 23))
     idx = vsg.Index(dim, "l2sq", connectivity=16, expansion_add=64, expansion_search=48, seed=7)
     idx.import_graph(h.export())
+    monkeypatch.setenv("VSG_SEARCH_REG", "0")
     monkeypatch.setenv("VSG_SEARCH_WAVES", waves)
     for ef, factor in ((10, "6"), (128, "6"), (400, "1"), (1024, "12")):
         monkeypatch.setenv("VSG_SEARCH_HASH_FACTOR", factor)
@@ -469,5 +473,45 @@ def test_hnsw_cooperative_search_bitexact(waves, monkeypatch):
         a1 = b.search(qf, 10, ef)
         monkeypatch.setenv("VSG_SEARCH_WAVES", waves)
         a2 = b.search(qf, 10, ef)
+        np.testing.assert_array_equal(a1.keys, a2.keys)
+        np.testing.assert_array_equal(a1.distances, a2.distances)
+
+
+@pytest.mark.parametrize("metric,dim,M", [("l2sq", 64, 16), ("ip", 32, 8)])
+def test_hnsw_register_search_bitexact(metric, dim, M, monkeypatch):
+    """Register-resident candidate set (hnsw_search_reg_kernel): bit-exact vs
+    the oracle on integer data for every register-row class (ef 10..1024),
+    with tombstones, k == ef, and a forgetful visited table (re-evaluated ids
+    de-duplicated against the set); identical to the LDS-list kernel on a
+    GPU-built float graph."""
+    n = 7000
+    x = G.uint8_valued(n, dim, 61) / (16.0 if metric == "ip" else 1.0)
+    q = G.uint8_valued(90, dim, 62) / (16.0 if metric == "ip" else 1.0)
+    h = O.HnswOracle(dim, metric, M, 64, 48, seed=9)
+    h.add(np.arange(n), x.astype(np.float32))
+    h.remove(np.arange(0, n, 13))
+    idx = vsg.Index(dim, metric, connectivity=M, expansion_add=64, expansion_search=48, seed=9)
+    idx.import_graph(h.export())
+    monkeypatch.setenv("VSG_SEARCH_REG", "1")
+    for ef, k, factor in ((10, 10, "6"), (48, 10, "6"), (64, 64, "6"), (100, 10, "1"), (192, 50, "6"),
+                          (400, 10, "1"), (448, 100, "12"), (700, 10, "6"), (1024, 1024, "12")):
+        monkeypatch.setenv("VSG_SEARCH_HASH_FACTOR", factor)
+        ok, od, oc = h.search(q, k, ef)
+        m = idx.search(q, k, ef)
+        np.testing.assert_array_equal(m.counts, oc)
+        np.testing.assert_array_equal(m.keys, ok)
+        np.testing.assert_array_equal(m.distances, od)
+    monkeypatch.delenv("VSG_SEARCH_HASH_FACTOR")
+    xf = G.clustered(9000, 96, 63, 4)
+    qf = G.clustered(300, 96, 64, 4)
+    b = vsg.Index(96, "cos", connectivity=16, expansion_add=64, expansion_search=64, seed=4)
+    b.add(np.arange(len(xf)), xf)
+    b.remove(np.arange(0, len(xf), 7))
+    for ef in (16, 64, 150, 300, 900):
+        monkeypatch.setenv("VSG_SEARCH_REG", "0")
+        a1 = b.search(qf, 10, ef)
+        monkeypatch.setenv("VSG_SEARCH_REG", "1")
+        a2 = b.search(qf, 10, ef)
+        np.testing.assert_array_equal(a1.counts, a2.counts)
         np.testing.assert_array_equal(a1.keys, a2.keys)
         np.testing.assert_array_equal(a1.distances, a2.distances)

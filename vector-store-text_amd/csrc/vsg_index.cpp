@@ -798,13 +798,19 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
             // visited table: LDS is the occupancy limit at large ef, and a
             // forgotten node costs one more row read -- cheap for short rows
             const bool wide = h->row_bytes >= 1024;
-            const int factor = (int)env_double("VSG_SEARCH_HASH_FACTOR", wide ? 12 : 6);
+            const bool reg = env_double("VSG_SEARCH_REG", 1) != 0;
+            // register kernel: sweep in profiles/r01_search_hash_reg.jsonl
+            const int factor = (int)env_double("VSG_SEARCH_HASH_FACTOR", wide ? (reg ? 8 : 12) : (reg ? 4 : 6));
             p.hash_size = std::max(hash_size_for(p.ef, factor), wide ? 2048 : 1024);
         }
         // waves per query: 1 = hnsw_search_kernel; 2 / 4 = cooperative kernel
         // (large ef, where one wave is latency-bound on the list).  Same results;
         // measured +5-7% at ef >= 321 (profiles/r01_search_waves.jsonl).
         p.waves = (int)env_double("VSG_SEARCH_WAVES", p.ef >= 256 ? 2 : 1);
+        // candidate set in registers (hnsw_search_reg.hip, default: same results,
+        // +12-46% at ef >= 192, profiles/r01_search_phases.jsonl);
+        // VSG_SEARCH_REG=0 selects the LDS-list kernels
+        p.reg = env_double("VSG_SEARCH_REG", 1) != 0 ? 1 : 0;
         err = launch_search(h->st, h->mk, p, s);
     } else if (err == hipSuccess) {
         ExactParams ep{};

@@ -34,6 +34,7 @@ struct SearchParams {
     int xcd_map;                // 1: workgroups b, b+8, ... (one XCD) take consecutive queries
     int hash_size;              // visited-table entries (hash_size_for)
     int waves;                  // waves per query: 1 (hnsw_search_kernel), 2 or 4 (cooperative)
+    int reg;                    // 1: hnsw_search_reg_kernel (candidate set in VGPRs; ignores waves)
 };
 
 struct InsertParams {
@@ -115,6 +116,8 @@ size_t search_lds_bytes(int ef, int hash, int waves = 1);
 size_t insert_lds_bytes(int efc, int hash);
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
+hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
+size_t search_reg_lds_bytes(int hash);
 hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s);
 hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s);
 hipError_t launch_exact(Storage st, MetricKind mk, const ExactParams& p, hipStream_t s);

@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "vector-store-text_amd"))
 def main():
     rows, dim, metric, quant, data = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
     efs = [int(e) for e in sys.argv[6].split(",")]
-    waves = sys.argv[7].split(",")  # "1", "2", "4": LDS-list kernels; "r": register kernel
+    waves = sys.argv[7].split(",")  # "1", "2", "4": LDS-list kernels; "r": register kernel; "s": + runner-up; "v": + bucketed visited; "w": both
     import torch
     import vsg
 
@@ -39,8 +39,10 @@ def main():
     for ef in efs:
         base = None
         for w in waves:
-            os.environ["VSG_SEARCH_REG"] = "1" if w == "r" else "0"
-            os.environ["VSG_SEARCH_WAVES"] = "1" if w == "r" else w
+            os.environ["VSG_SEARCH_REG"] = "1" if w in "rsvw" else "0"
+            os.environ["VSG_SEARCH_SPEC"] = "1" if w in "sw" else "0"
+            os.environ["VSG_SEARCH_VIS8"] = "1" if w in "vw" else "0"
+            os.environ["VSG_SEARCH_WAVES"] = "1" if w in "rsvw" else w
             kk, dd = idx.search_device(q, 10, ef)[:2]
             kk, dd = kk.cpu().numpy(), dd.cpu().numpy()
             if base is None:
@@ -62,7 +64,7 @@ def main():
                      "expansions_per_query": round(st["search_adjacency"] / nq, 1)}
             if raw[10] or raw[11]:  # profiling build: wave-microseconds per query per phase
                 extra.update({f"us_{k}": round(raw[i] / 100.0 / nq, 2) for k, i in (("adj", 10), ("dist", 11), ("merge", 12))})
-            print(json.dumps({"rows": rows, "dim": dim, "metric": metric, "quant": quant, "ef": ef, "kernel": "reg" if w == "r" else f"list{w}",
+            print(json.dumps({"rows": rows, "dim": dim, "metric": metric, "quant": quant, "ef": ef, "kernel": {"r": "reg", "s": "reg+spec", "v": "reg+vis8", "w": "reg+vis8+spec"}.get(w, f"list{w}"),
                               "build_s": round(bt, 2), "qps": round(10000 / dt, 1), "recall": round(rec, 4),
                               "same_as_1wave": same, **extra}), flush=True)
 

@@ -198,9 +198,42 @@ template <int R> struct RegSet {
     }
 };
 
+// Admit this lane's candidate key `ck` if `mine` (one expansion's batch).
+template <int R>
+__device__ __forceinline__ void admit(RegSet<R>& B, bool mine, uint64_t ck, bool lossy, int ef, uint64_t* sk) {
+    const int lane = lane_id();
+    bool valid = mine && ck < B.tkey;
+    uint64_t vm = __ballot(valid);
+    if (lossy && vm) {
+        // a forgotten id evaluated again: drop it if B still holds it
+        for (uint64_t mm = vm; mm; mm &= mm - 1) {
+            const int j = __builtin_ctzll(mm);
+            if (B.contains(readlane64(ck, j))) vm &= ~(1ull << j);
+        }
+        valid = (vm >> lane) & 1ull;
+    }
+    int nc = popc64(vm);
+    if (nc && B.size + nc > 64 * R) {
+        B.compact(ef);
+        valid = valid && ck < B.tkey;
+        vm = __ballot(valid);
+        nc = popc64(vm);
+    }
+    if (nc) {
+        if (valid) sk[lanes_below(vm)] = ck;
+        wave_sync();
+        B.fill(sk, nc);
+        wave_sync();
+    }
+}
+
+// Level-0 beam (oracle beam() on level 0).  Preparing the runner-up expansion
+// alongside (its adjacency row and distances in the same round trips,
+// committed only when it is the sequential next step) was measured 0-15%
+// slower: the runner-up is rarely still next (profiles/r01_search_phases.jsonl).
 template <int G, int VM, int U, typename T, int MET, int R>
-__device__ void beam0_reg(const GraphDev& g, const QReg<G, VM, T>& q, uint32_t ep, float dep, int ef,
-                          WaveLds& w, RegSet<R>& B, uint64_t& ndist, uint64_t& nadj, BeamProf& pf) {
+__device__ void beam0_reg(const GraphDev& g, const QReg<G, VM, T>& q, uint32_t ep, float dep, int ef, WaveLds& w,
+                          RegSet<R>& B, uint64_t& ndist, uint64_t& nadj, BeamProf& pf) {
     const int lane = lane_id();
     const int m = g.M0;
     w.vis.clear();
@@ -214,12 +247,11 @@ __device__ void beam0_reg(const GraphDev& g, const QReg<G, VM, T>& q, uint32_t e
     wave_sync();
     for (;;) {
         const uint64_t t0 = VSG_CLK();
-        const uint64_t best = B.min_unexpanded();
-        if (best == VSG_KEY_EMPTY) break;
-        if (B.size > ef && B.count_below(best) >= ef) break;
-        B.mark_expanded(best);
-        const uint32_t node = (uint32_t)best & VSG_ID_MASK;
-        const uint32_t* row = g.row(node, 0);
+        const uint64_t a = B.min_unexpanded();
+        if (a == VSG_KEY_EMPTY) break;
+        if (B.size > ef && B.count_below(a) >= ef) break;
+        B.mark_expanded(a);
+        const uint32_t* row = g.row((uint32_t)a & VSG_ID_MASK, 0);
         const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
         ++nadj;
         bool fresh = false, evicted = false;
@@ -238,29 +270,7 @@ __device__ void beam0_reg(const GraphDev& g, const QReg<G, VM, T>& q, uint32_t e
         const uint64_t ck = lane < cnt ? cand_key(w.tdist[lane], w.todo[lane]) : VSG_KEY_EMPTY;
         const uint64_t t2 = VSG_CLK();
         pf.dist += t2 - t1;
-        bool valid = ck < B.tkey;
-        uint64_t vm = __ballot(valid);
-        if (lossy && vm) {
-            // a forgotten id evaluated again: drop it if B still holds it
-            for (uint64_t mm = vm; mm; mm &= mm - 1) {
-                const int j = __builtin_ctzll(mm);
-                if (B.contains(readlane64(ck, j))) vm &= ~(1ull << j);
-            }
-            valid = (vm >> lane) & 1ull;
-        }
-        int nc = popc64(vm);
-        if (nc && B.size + nc > 64 * R) {
-            B.compact(ef);
-            valid = valid && ck < B.tkey;
-            vm = __ballot(valid);
-            nc = popc64(vm);
-        }
-        if (nc) {
-            if (valid) sk[lanes_below(vm)] = ck;
-            wave_sync();
-            B.fill(sk, nc);
-            wave_sync();
-        }
+        admit<R>(B, lane < cnt, ck, lossy, ef, sk);
         pf.merge += VSG_CLK() - t2;
     }
 }

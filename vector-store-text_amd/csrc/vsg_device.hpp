@@ -157,7 +157,7 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
 
 struct Visited {
     uint32_t* tab;
-    uint32_t size;  // entries (multiple of 4, any value: slots via multiply-high)
+    uint32_t size;  // entries (multiple of 8; buckets via multiply-high)
 
     __device__ __forceinline__ void clear() {
         const int lane = lane_id();
@@ -167,29 +167,50 @@ struct Visited {
         wave_sync();
     }
 
-    // true if id was not present (it is recorded now).  A table that is too
-    // small forgets: after PROBES occupied slots the id overwrites its home slot
-    // and `evicted` is set; from then on the caller must treat every fresh id as
-    // possibly seen before and de-duplicate against the top-ef list.  Forgetting
-    // never changes the traversal, it only adds distance evaluations: a node seen
-    // before is either still in the list (de-duplicated there) or worse than the
-    // list's current worst entry (rejected by the merge threshold; entries only
-    // leave a full list).
-    template <int PROBES = 16>
+    // true if id was not present (it is recorded now).  The id's home is an
+    // aligned bucket of 8 slots, read with two 16-B LDS loads; a free slot is
+    // claimed with one CAS (re-read if another lane took it).  A table that is
+    // too small forgets: a full bucket overwrites one of its ids (slot chosen
+    // by the new id) and `evicted` is set; from then on the caller must treat
+    // every fresh id as possibly seen before and de-duplicate against the
+    // top-ef set.  Forgetting never changes the traversal, it only adds
+    // distance evaluations: a node seen before is either still in the top-ef
+    // set (de-duplicated there) or worse than its current worst entry
+    // (rejected by the admission threshold; entries only leave a full set).
+    // One LDS round trip + one atomic per id (linear probing needed up to 16
+    // dependent atomics once the table was crowded: profiles/r01_search_phases.jsonl).
     __device__ __forceinline__ bool insert(uint32_t id, bool& evicted) {
-        const uint32_t h0 = __umulhi(id * 2654435761u, size);
-        uint32_t h = h0;
+        const uint32_t b0 = __umulhi(id * 2654435761u, size >> 3) << 3;
+        const uint4* t4 = reinterpret_cast<const uint4*>(tab + b0);
         evicted = false;
 #pragma unroll 1
-        for (int p = 0; p < PROBES; ++p) {
-            const uint32_t old = atomicCAS(&tab[h], VSG_EMPTY, id);
+        for (int attempt = 0; attempt < 8; ++attempt) {
+            const uint4 x = t4[0], y = t4[1];
+            const uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+            int fs = -1;
+            bool hit = false;
+#pragma unroll
+            for (int i = 7; i >= 0; --i) {
+                hit = hit || v[i] == id;
+                if (v[i] == VSG_EMPTY) fs = i;
+            }
+            if (hit) return false;
+            if (fs < 0) break;
+            const uint32_t old = atomicCAS(&tab[b0 + fs], VSG_EMPTY, id);
             if (old == VSG_EMPTY) return true;
             if (old == id) return false;
-            h = h + 1 == size ? 0 : h + 1;
         }
-        atomicExch(&tab[h0], id);
+        atomicExch(&tab[b0 + (id & 7)], id);
         evicted = true;
         return true;
+    }
+
+    // lookup only: !insert() without recording
+    __device__ __forceinline__ bool contains(uint32_t id) const {
+        const uint32_t b0 = __umulhi(id * 2654435761u, size >> 3) << 3;
+        const uint4* t4 = reinterpret_cast<const uint4*>(tab + b0);
+        const uint4 x = t4[0], y = t4[1];
+        return x.x == id || x.y == id || x.z == id || x.w == id || y.x == id || y.y == id || y.z == id || y.w == id;
     }
 };
 

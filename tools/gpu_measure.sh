@@ -8,7 +8,7 @@ rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
 [ $rc -ne 0 ] && exit $rc
 EF=$(python -c "import json;print(json.loads(open('gpurun_out/bench.log').read().strip().splitlines()[-1])['config']['ef'])")
 echo "ef=$EF"
-ARGS="--no-cpu --ef $EF --steps 3 --warmup 1"
+ARGS="--no-cpu --ef $EF --config-ef 0 --steps 3 --warmup 1"
 rm -rf gpurun_out/prof gpurun_out/pmc_fetch gpurun_out/pmc_write
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py $ARGS > gpurun_out/prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -1 gpurun_out/prof.log; [ $rc -ne 0 ] && exit $rc

@@ -26,7 +26,7 @@ def per_dispatch(d, counter):
     vals = defaultdict(float)
     grid = {}
     for r in csv.DictReader(open(files[0])):
-        if r.get("Counter_Name") != counter or "hnsw_search_kernel" not in r.get("Kernel_Name", ""):
+        if r.get("Counter_Name") != counter or "hnsw_search_" not in r.get("Kernel_Name", ""):
             continue
         key = r.get("Dispatch_Id") or r.get("Correlation_Id")
         vals[key] += float(r["Counter_Value"])
@@ -47,7 +47,7 @@ def main():
     write_kib = sum(wv[k] for k in fullw) / max(1, len(fullw))
     out = {
         "workload": {"n": int(n), "dim": int(dim), "queries": nq, "ef": int(ef), "metric": metric},
-        "kernel": "hnsw_search_kernel",
+        "kernel": "hnsw_search_reg_kernel",
         "dispatches": len(full),
         "fetch_size_kib_raw": round(fetch_kib, 1),
         "write_size_kib_raw": round(write_kib, 1),

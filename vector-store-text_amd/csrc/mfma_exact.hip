@@ -5,10 +5,9 @@
 // fused with a per-lane register top-KMAX so no distance tile ever reaches HBM.
 //
 //   block = 256 threads (4 waves, 2 x 2), tile = 128 base rows x 128 queries,
-//   K stage = 32 dims, double-buffered LDS [rows | queries][32 + 4 pad] floats
-//   (row stride 36 dwords: the 16-lane groups of ds_read_b128 hit disjoint banks),
-//   register-staged global loads issued before the MFMAs of the current stage
-//   and written to the other LDS buffer after them (one barrier per stage).
+//   K stage = 32 dims, two static LDS buffers [rows | queries][32] floats (64 KiB,
+//   XOR-swizzled 16-B slots), the next stage streamed in by LDS-DMA
+//   (global_load_lds) during the MFMAs of the current one, one barrier per stage.
 //   Wave (wr, wq) owns rows [wr*64, +64) x queries [wq*64, +64) = 2 x 2 MFMA tiles.
 //   A operand = base rows, B operand = queries, so C lane l holds query (l & 31)
 //   against 16 rows: each lane keeps a sorted top-KMAX per query in VGPRs.
@@ -31,7 +30,6 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int KT = 32;   // dims per stage = one 128-B LDS row
 constexpr int LDK = 32;  // LDS row stride (floats), unpadded: glds writes lane-linear 1-KiB pieces
 constexpr int STAGE_FLOATS = (MFMA_BR + MFMA_BQ) * LDK;
-constexpr size_t MFMA_LDS_BYTES = 2 * STAGE_FLOATS * sizeof(float);
 
 // 16-B slot of logical chunk c (0..7) in LDS row R: XOR swizzle so the sixteen
 // lanes of a ds_read_b128 group (rows R..R+15, same chunk) hit distinct slots of
@@ -59,7 +57,8 @@ __device__ __forceinline__ void topk_insert(float (&ld)[KMAX], uint32_t (&li)[KM
 
 template <int KMAX, int MET>
 __global__ __launch_bounds__(256, 2) void mfma_exact_kernel(MfmaExactParams p) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ __attribute__((aligned(16))) float lds_a[STAGE_FLOATS];
+    __shared__ __attribute__((aligned(16))) float lds_b[STAGE_FLOATS];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int w = tid >> 6;
@@ -112,9 +111,8 @@ __global__ __launch_bounds__(256, 2) void mfma_exact_kernel(MfmaExactParams p) {
         // base-row and query tiles; out-of-range rows read a clamped valid row
         // (masked in the epilogue / never written out).
         const int prow = lane >> 3, pslot = lane & 7;
-        auto load_stage = [&](int s, int buf) {
+        auto load_stage = [&](int s, float* xs) {
             const int k0 = s * KT;
-            float* xs = lds + buf * STAGE_FLOATS;
             float* qs = xs + MFMA_BR * LDK;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -129,14 +127,15 @@ __global__ __launch_bounds__(256, 2) void mfma_exact_kernel(MfmaExactParams p) {
                                                  (lptr_t)(qs + piece * 8 * LDK), 16, 0, 0);
             }
         };
-
-        load_stage(0, 0);
-        __syncthreads();  // drains the LDS-DMA (vmcnt(0)) and publishes stage 0
-        for (int s = 0; s < nst; ++s) {
-            const int buf = s & 1;
-            if (s + 1 < nst) load_stage(s + 1, buf ^ 1);  // buf^1 was last read before the previous barrier
-            const float* xs = lds + buf * STAGE_FLOATS;
-            const float* qs = xs + MFMA_BR * LDK;
+        // one K stage: MFMAs on `cur` while the next stage streams into `nxt`.
+        // cur / nxt are two distinct __shared__ arrays named statically (the loop
+        // is unrolled by two), so the compiler can tell the DMA target from the
+        // ds_read source; through one runtime-indexed buffer it waited for the
+        // DMA (vmcnt(0)) before the stage's first ds_read.
+        auto stage = [&](int s, const float* cur, float* nxt) __attribute__((always_inline)) {
+            if (s + 1 < nst) load_stage(s + 1, nxt);  // nxt was last read before the previous barrier
+            const float* xs = cur;
+            const float* qs = cur + MFMA_BR * LDK;
 #pragma unroll
             for (int tq = 0; tq < 4; ++tq) {
                 float4 xa[2], qb[2];
@@ -163,6 +162,13 @@ __global__ __launch_bounds__(256, 2) void mfma_exact_kernel(MfmaExactParams p) {
                 }
             }
             __syncthreads();
+        };
+
+        load_stage(0, lds_a);
+        __syncthreads();  // drains the LDS-DMA (vmcnt(0)) and publishes stage 0
+        for (int s = 0; s < nst; s += 2) {
+            stage(s, lds_a, lds_b);
+            if (s + 1 < nst) stage(s + 1, lds_b, lds_a);
         }
 
         // epilogue: distances + register top-KMAX (rows arrive in increasing slot order)
@@ -205,8 +211,7 @@ hipError_t launch_mfma_exact(MetricKind mk, const MfmaExactParams& p, hipStream_
     const int total = p.qtiles * p.splits;
     const int nb = (total + 7) / 8 * 8;
     auto kern = mk == MK_L2 ? mfma_exact_kernel<16, MET_L2> : mfma_exact_kernel<16, MET_DOT>;
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)MFMA_LDS_BYTES);
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(256), MFMA_LDS_BYTES, s, p);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

@@ -189,7 +189,7 @@ def hnsw_leg(c, mode):
         ef = a.ef
         sweep.append((ef, recall_of(search(qgt, ef, kshard(ef))[0])))
     else:
-        grid = (4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512)
+        grid = (4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024)
         if not sharded:
             grid = tuple(e for e in grid if e >= max(16, a.k))
         ef, lo_fail = None, None

@@ -46,6 +46,9 @@ def main():
         wall = {"insert_wave_us_avg": round(raw[10] / rows / 100, 1), "insert_wave_us_max": round(raw[11] / 100, 1),
                 "reverse_wave_us_sum_ms": round(raw[12] / 1e5, 1), "reverse_wave_us_max": round(raw[13] / 100, 1),
                 "batches": st["build_batches"]}
+        if raw[14] or raw[15]:  # profiling build: insert-wave beam phases per vector
+            wall.update({"insert_beam_adj_dist_us": round(raw[15] / rows / 100, 1),
+                         "insert_beam_merge_us": round(raw[14] / rows / 100, 1)})
         h = hashlib.sha1(ex["adj0"].tobytes())
         h.update(ex["upper"].tobytes())
         print(json.dumps({"rows": rows, "dim": dim, "cfg": cfg, "build_s": round(bt, 3),

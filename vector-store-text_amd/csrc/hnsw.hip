@@ -106,11 +106,15 @@ __device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uin
     const int lane = lane_id();
     List& L = w.list;
     int kept = 0;
+    // the next candidate's row streams in while this one is tested
+    uint4 raw[VM];
+    if (n > 0) QReg<G, VM, T>::fetch(g.vec(L.I()[0] & VSG_ID_MASK), g.nchunks, raw);
     for (int i = 0; i < n && kept < m; ++i) {
         const uint32_t c = L.I()[i] & VSG_ID_MASK;
         const float cdist = L.D()[i];
         QReg<G, VM, T> cq;
-        cq.load(g.vec(c), g.nchunks);
+        cq.set(raw, g.nchunks);
+        if (i + 1 < n) QReg<G, VM, T>::fetch(g.vec(L.I()[i + 1] & VSG_ID_MASK), g.nchunks, raw);
         bool good = true;
         for (int b = 0; b < kept; b += BLK) {
             const int cnt = min(BLK, kept - b);
@@ -412,6 +416,10 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
         const unsigned long long dt = wall_clock64() - t_start;
         atomicAdd(&p.stats[10], dt);
         atomicMax(&p.stats[11], dt);
+#ifdef VSG_SEARCH_PROFILE
+        atomicAdd(&p.stats[14], (unsigned long long)pf.merge);
+        atomicAdd(&p.stats[15], (unsigned long long)(pf.adj + pf.dist));
+#endif
     }
 }
 

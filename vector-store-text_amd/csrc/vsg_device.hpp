@@ -100,6 +100,39 @@ template <int G, int VM, typename T> struct QReg {
             }
         }
     }
+
+    // split load: fetch() issues the 16-B loads into `raw` (no use, so no wait),
+    // set() converts them later -- lets a row stream in under other work
+    __device__ __forceinline__ static void fetch(const uint8_t* __restrict__ row, int nchunks, uint4 (&raw)[VM]) {
+        const int sl = lane_id() % G;
+#pragma unroll
+        for (int v = 0; v < VM; ++v) {
+            const int c = v * G + sl;
+            const int cc = c < nchunks ? c : nchunks - 1;
+            raw[v] = *reinterpret_cast<const uint4*>(row + (size_t)cc * 16);
+        }
+    }
+    __device__ __forceinline__ void set(const uint4 (&raw)[VM], int nchunks) {
+        const int sl = lane_id() % G;
+#pragma unroll
+        for (int v = 0; v < VM; ++v) {
+            const int c = v * G + sl;
+            if constexpr (sizeof(T) == 4) {
+                x[v][0] = __uint_as_float(raw[v].x);
+                x[v][1] = __uint_as_float(raw[v].y);
+                x[v][2] = __uint_as_float(raw[v].z);
+                x[v][3] = __uint_as_float(raw[v].w);
+            } else {
+                half8_t h = __builtin_bit_cast(half8_t, raw[v]);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) x[v][e] = (float)h[e];
+            }
+            if (c >= nchunks) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) x[v][e] = 0.f;
+            }
+        }
+    }
 };
 
 // Distances from the register image q to `count` rows listed in ids[] (LDS),

@@ -102,37 +102,67 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
 // keep c unless a kept r has dist(c, r) < dist(c, base).  Returns #kept.
 template <int G, int VM, int U, typename T, int MET>
 __device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uint64_t& ndist) {
+    // Candidates go in pairs (c0, c1): both are tested against the kept set in
+    // one pass over its rows (each row loaded once, rows_dist2); c1 is then
+    // also tested against c0 if c0 was kept -- the sequential decision for
+    // both, with the same distance values.  The next pair's rows stream in
+    // under the current tests.
     constexpr int BLK = (64 / G) * U;
     const int lane = lane_id();
     List& L = w.list;
     int kept = 0;
-    // the next candidate's row streams in while this one is tested
-    uint4 raw[VM];
-    if (n > 0) QReg<G, VM, T>::fetch(g.vec(L.I()[0] & VSG_ID_MASK), g.nchunks, raw);
-    for (int i = 0; i < n && kept < m; ++i) {
-        const uint32_t c = L.I()[i] & VSG_ID_MASK;
-        const float cdist = L.D()[i];
-        QReg<G, VM, T> cq;
-        cq.set(raw, g.nchunks);
-        if (i + 1 < n) QReg<G, VM, T>::fetch(g.vec(L.I()[i + 1] & VSG_ID_MASK), g.nchunks, raw);
-        bool good = true;
-        for (int b = 0; b < kept; b += BLK) {
+    using Q = QReg<G, VM, T>;
+    uint4 raw0[VM], raw1[VM];
+    if (n > 0) Q::fetch(g.vec(L.I()[0] & VSG_ID_MASK), g.nchunks, raw0);
+    if (n > 1) Q::fetch(g.vec(L.I()[1] & VSG_ID_MASK), g.nchunks, raw1);
+    float* d1out = w.sd;  // 64-entry scratch beside tdist
+    for (int i = 0; i < n && kept < m; i += 2) {
+        const bool two = i + 1 < n;
+        const uint32_t c0 = L.I()[i] & VSG_ID_MASK;
+        const float cd0 = L.D()[i];
+        const uint32_t c1 = two ? (L.I()[i + 1] & VSG_ID_MASK) : 0u;
+        const float cd1 = two ? L.D()[i + 1] : 0.f;
+        Q q0, q1;
+        q0.set(raw0, g.nchunks);
+        q1.set(raw1, g.nchunks);
+        if (i + 2 < n) Q::fetch(g.vec(L.I()[i + 2] & VSG_ID_MASK), g.nchunks, raw0);
+        if (i + 3 < n) Q::fetch(g.vec(L.I()[i + 3] & VSG_ID_MASK), g.nchunks, raw1);
+        bool good0 = true, good1 = two;
+        for (int b = 0; b < kept && (good0 || good1); b += BLK) {
             const int cnt = min(BLK, kept - b);
-            rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.sel + b, cnt, cq, w.tdist);
-            wave_sync();
-            ndist += (uint64_t)cnt;
-            const bool bad = lane < cnt && w.tdist[lane] < cdist;
-            const uint64_t bm = __ballot(bad);
-            wave_sync();
-            if (bm) {
-                good = false;
-                break;
+            if (good1) {
+                rows_dist2<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.sel + b, cnt, q0, q1, w.tdist, d1out);
+                ndist += 2 * (uint64_t)cnt;
+            } else {
+                rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.sel + b, cnt, q0, w.tdist);
+                ndist += (uint64_t)cnt;
             }
+            wave_sync();
+            if (good0 && __ballot(lane < cnt && w.tdist[lane] < cd0)) good0 = false;
+            if (good1 && __ballot(lane < cnt && d1out[lane] < cd1)) good1 = false;
+            wave_sync();
         }
-        if (good) {
+        if (good0) {
             if (lane == 0) {
-                w.sel[kept] = c;
-                w.seld[kept] = cdist;
+                w.sel[kept] = c0;
+                w.seld[kept] = cd0;
+            }
+            ++kept;
+            wave_sync();
+        }
+        if (!two || kept >= m || !good1) continue;
+        if (good0) {
+            // c1 against the just-kept c0
+            rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.sel + kept - 1, 1, q1, w.tdist);
+            wave_sync();
+            ++ndist;
+            good1 = !(w.tdist[0] < cd1);
+            wave_sync();
+        }
+        if (good1) {
+            if (lane == 0) {
+                w.sel[kept] = c1;
+                w.seld[kept] = cd1;
             }
             ++kept;
             wave_sync();

@@ -186,6 +186,67 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
     }
 }
 
+// rows_dist for two register images at once: each row is loaded once and
+// reduced against both (out0 from q0, out1 from q1; same values as two
+// rows_dist calls).
+template <int G, int VM, int U, typename T, int MET>
+__device__ __forceinline__ void rows_dist2(const uint8_t* __restrict__ vecs, size_t row_bytes, int nchunks,
+                                           const uint32_t* ids, int count, const QReg<G, VM, T>& q0,
+                                           const QReg<G, VM, T>& q1, float* out0, float* out1) {
+    constexpr int R = 64 / G;
+    constexpr int E = ChunkT<T>::E;
+    const int lane = lane_id();
+    const int sub = lane / G;
+    const int sl = lane % G;
+    for (int base = 0; base < count; base += R * U) {
+        float buf[U][VM][E];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = base + u * R + sub;
+            const int rr = r < count ? r : count - 1;
+            const uint8_t* row = vecs + (size_t)ids[rr] * row_bytes;
+#pragma unroll
+            for (int v = 0; v < VM; ++v) {
+                const int c = v * G + sl;
+                load_chunk<T>(row, c < nchunks ? c : nchunks - 1, buf[u][v]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+            for (int v = 0; v < VM; ++v) {
+                const bool live = (v * G + sl) < nchunks;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    float t0, t1;
+                    if constexpr (MET == MET_L2) {
+                        const float d0 = buf[u][v][e] - q0.x[v][e];
+                        const float d1 = buf[u][v][e] - q1.x[v][e];
+                        t0 = d0 * d0;
+                        t1 = d1 * d1;
+                    } else {
+                        t0 = buf[u][v][e] * q0.x[v][e];
+                        t1 = buf[u][v][e] * q1.x[v][e];
+                    }
+                    a0 += live ? t0 : 0.f;
+                    a1 += live ? t1 : 0.f;
+                }
+            }
+#pragma unroll
+            for (int o = G / 2; o > 0; o >>= 1) {
+                a0 += __shfl_xor(a0, o);
+                a1 += __shfl_xor(a1, o);
+            }
+            const int r = base + u * R + sub;
+            if (sl == 0 && r < count) {
+                out0[r] = (MET == MET_L2) ? a0 : 1.f - a0;
+                out1[r] = (MET == MET_L2) ? a1 : 1.f - a1;
+            }
+        }
+    }
+}
+
 // ----------------------------------------------------------------- visited --
 
 struct Visited {

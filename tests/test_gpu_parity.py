@@ -515,3 +515,36 @@ def test_hnsw_register_search_bitexact(metric, dim, M, monkeypatch):
         np.testing.assert_array_equal(a1.counts, a2.counts)
         np.testing.assert_array_equal(a1.keys, a2.keys)
         np.testing.assert_array_equal(a1.distances, a2.distances)
+
+
+def test_full_size_c2_kernels_agree(monkeypatch):
+    """BASELINE configs[1] at full size (1M x 768 f32 cos, data generated in
+    HBM): the register-set kernel, the LDS-list kernel and the cooperative
+    kernel return identical keys and distances at the bench's ef and at the
+    config's ef=128; results are sorted and recall@10 >= 0.95 at ef=48."""
+    torch = pytest.importorskip("torch")
+    n, dim = 1_000_000, 768
+    bs, qs, ms = G.config_seeds(1)
+    x = vsg.datagen_device("clustered", n, dim, bs, ms)
+    q = vsg.datagen_device("clustered", 2000, dim, qs, ms)
+    idx = vsg.Index(dim, "cos", "f32", 16, 128, 64, seed=0x5EED)
+    idx.reserve(n)
+    idx.add_device(np.arange(n, dtype=np.uint64), x)
+    del x
+    gt = idx.search_device(q, 10, exact=True)[0].cpu().numpy()
+    for ef in (36, 128):
+        res = {}
+        for name, env in (("reg", {"VSG_SEARCH_REG": "1"}), ("list", {"VSG_SEARCH_REG": "0", "VSG_SEARCH_WAVES": "1"}),
+                          ("wg2", {"VSG_SEARCH_REG": "0", "VSG_SEARCH_WAVES": "2"})):
+            for k_, v_ in env.items():
+                monkeypatch.setenv(k_, v_)
+            kk, dd = idx.search_device(q, 10, ef)[:2]
+            res[name] = (kk.cpu().numpy(), dd.cpu().numpy())
+        for name in ("list", "wg2"):
+            np.testing.assert_array_equal(res["reg"][0], res[name][0])
+            np.testing.assert_array_equal(res["reg"][1], res[name][1])
+        assert (np.diff(res["reg"][1], axis=1) >= 0).all()
+    monkeypatch.setenv("VSG_SEARCH_REG", "1")
+    k48 = idx.search_device(q, 10, 48)[0].cpu().numpy()
+    assert recall(k48, gt, 10) >= 0.95
+    torch.cuda.synchronize()

@@ -17,6 +17,7 @@
 #include "vsg_dispatch.hpp"
 #include "vsg_kernels.hpp"
 #include "hnsw_common.hpp"
+#include "hnsw_regset.hpp"
 
 namespace vsg {
 
@@ -423,7 +424,15 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     for (int l = p.max_level; l > L; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
     uint32_t pos = p.pair_off[bi];
     for (int l = min(L, p.max_level); l >= 0; --l) {
-        beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, pf);
+        if (p.efc <= 192) {
+            // candidate set in VGPRs (hnsw_regset.hpp), then the sorted top-efc
+            // list the selection walks -- the list beam's exact result
+            RegSet<4> B;
+            beam_reg<G, VM, U, T, MET, 4>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf);
+            regset_to_list<4>(B, p.efc, w);
+        } else {
+            beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, pf);
+        }
         const int m = l == 0 ? g.M0 : g.M;
         const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, m, nsel_d);
         uint32_t* row = g.row(node, l);

@@ -1,0 +1,295 @@
+// hnsw_regset.hpp — the HNSW beam with its candidate set in VGPRs (used by
+// hnsw_search_reg_kernel and by the insert kernel); see hnsw_search_reg.hip
+// for the argument that it expands the same nodes as the sorted-list beam.
+#pragma once
+#include "hnsw_common.hpp"
+
+namespace vsg {
+
+#define VSG_KEY_EMPTY (~0ull)
+
+// (distance, slot) -> key whose unsigned order is cand_less order (-0 == +0).
+__device__ __forceinline__ uint64_t cand_key(float d, uint32_t id) {
+    uint32_t b = __float_as_uint(d);
+    if (b == 0x80000000u) b = 0u;
+    const uint32_t u = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    return ((uint64_t)u << 32) | (id & VSG_ID_MASK);
+}
+__device__ __forceinline__ float key_dist(uint64_t k) {
+    const uint32_t u = (uint32_t)(k >> 32);
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int o) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = shfl_xor64(v, o);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int R> struct RegSet {
+    uint64_t k[R];   // slot r of this lane; VSG_KEY_EMPTY = free
+    uint32_t expm;   // bit r: slot r expanded
+    int size;        // occupied slots (wave-uniform)
+    uint64_t tkey;   // admission bound (wave-uniform)
+
+    __device__ __forceinline__ void init(uint64_t first) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) k[r] = VSG_KEY_EMPTY;
+        if (lane_id() == 0) k[0] = first;
+        expm = 0;
+        size = 1;
+        tkey = VSG_KEY_EMPTY;
+    }
+
+    // smallest unexpanded key (VSG_KEY_EMPTY if none)
+    __device__ __forceinline__ uint64_t min_unexpanded() const {
+        uint64_t b = VSG_KEY_EMPTY;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (!((expm >> r) & 1u) && k[r] < b) b = k[r];
+        return wave_min64(b);
+    }
+
+    // #keys below x (wave-uniform)
+    __device__ __forceinline__ int count_below(uint64_t x) const {
+        int c = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) c += popc64(__ballot(k[r] < x));
+        return c;
+    }
+
+    __device__ __forceinline__ void mark_expanded(uint64_t x) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (k[r] == x) expm |= 1u << r;
+    }
+
+    __device__ __forceinline__ bool contains(uint64_t x) const {
+        bool h = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) h = h || k[r] == x;
+        return __ballot(h) != 0;
+    }
+
+    // keep the `keep` smallest keys (size > keep); tkey = the largest kept.
+    // MSB-first radix select on the distance word: bit b of the answer is 0
+    // iff at least `need` keys share its higher bits and have 0 there.  The
+    // slot word is only selected on when several kept candidates tie on the
+    // cut distance (then `need` < their count).
+    __device__ __forceinline__ void compact(int keep) {
+        uint32_t ph = 0;
+        int need = keep;
+#pragma unroll 1
+        for (int b = 31; b >= 0; --b) {
+            const uint32_t hm = b == 31 ? 0u : (~0u << (b + 1));
+            int c = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t hi = (uint32_t)(k[r] >> 32);
+                c += popc64(__ballot(k[r] != VSG_KEY_EMPTY && (hi & hm) == ph && !((hi >> b) & 1u)));
+            }
+            if (c < need) {
+                need -= c;
+                ph |= 1u << b;
+            }
+        }
+        int ceq = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) ceq += popc64(__ballot(k[r] != VSG_KEY_EMPTY && (uint32_t)(k[r] >> 32) == ph));
+        uint64_t cut;
+        if (need == ceq) {
+            // every key on the cut distance stays: the cut is the largest of them
+            uint64_t mx = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (k[r] != VSG_KEY_EMPTY && (uint32_t)(k[r] >> 32) == ph && k[r] > mx) mx = k[r];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint64_t w = shfl_xor64(mx, o);
+                mx = w > mx ? w : mx;
+            }
+            cut = mx;
+        } else {
+            uint32_t pl = 0;
+#pragma unroll 1
+            for (int b = 31; b >= 0; --b) {
+                const uint32_t hm = b == 31 ? 0u : (~0u << (b + 1));
+                int c = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t lo = (uint32_t)k[r];
+                    c += popc64(__ballot(k[r] != VSG_KEY_EMPTY && (uint32_t)(k[r] >> 32) == ph && (lo & hm) == pl &&
+                                         !((lo >> b) & 1u)));
+                }
+                if (c < need) {
+                    need -= c;
+                    pl |= 1u << b;
+                }
+            }
+            cut = ((uint64_t)ph << 32) | pl;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (k[r] > cut) {
+                k[r] = VSG_KEY_EMPTY;
+                expm &= ~(1u << r);
+            }
+        size = keep;
+        tkey = cut;
+    }
+
+    // place the nc staged keys sk[0..nc) into free slots
+    __device__ __forceinline__ void fill(const uint64_t* sk, int nc) {
+        int acc = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (acc < nc) {
+                const bool fr = k[r] == VSG_KEY_EMPTY;
+                const uint64_t em = __ballot(fr);
+                const int idx = acc + lanes_below(em);
+                if (fr && idx < nc) {
+                    k[r] = sk[idx];
+                    expm &= ~(1u << r);
+                }
+                acc += popc64(em);
+            }
+        }
+        size += nc;
+    }
+};
+
+// Admit this lane's candidate key `ck` if `mine` (one expansion's batch).
+template <int R>
+__device__ __forceinline__ void admit(RegSet<R>& B, bool mine, uint64_t ck, bool lossy, int ef, uint64_t* sk) {
+    const int lane = lane_id();
+    bool valid = mine && ck < B.tkey;
+    uint64_t vm = __ballot(valid);
+    if (lossy && vm) {
+        // a forgotten id evaluated again: drop it if B still holds it
+        for (uint64_t mm = vm; mm; mm &= mm - 1) {
+            const int j = __builtin_ctzll(mm);
+            if (B.contains(readlane64(ck, j))) vm &= ~(1ull << j);
+        }
+        valid = (vm >> lane) & 1ull;
+    }
+    int nc = popc64(vm);
+    if (nc && B.size + nc > 64 * R) {
+        B.compact(ef);
+        valid = valid && ck < B.tkey;
+        vm = __ballot(valid);
+        nc = popc64(vm);
+    }
+    if (nc) {
+        if (valid) sk[lanes_below(vm)] = ck;
+        wave_sync();
+        B.fill(sk, nc);
+        wave_sync();
+    }
+}
+
+// Beam on level l (oracle beam()).  Preparing the runner-up expansion
+// alongside (its adjacency row and distances in the same round trips,
+// committed only when it is the sequential next step) was measured 0-15%
+// slower: the runner-up is rarely still next (profiles/r01_search_phases.jsonl).
+template <int G, int VM, int U, typename T, int MET, int R>
+__device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t ep, float dep, int ef, WaveLds& w,
+                         RegSet<R>& B, uint64_t& ndist, uint64_t& nadj, BeamProf& pf) {
+    const int lane = lane_id();
+    // select on values (readfirstlane), not on field addresses: a
+    // select-of-loads folded into a load-of-select pinned the graph
+    // descriptor in scratch inside the insert kernel
+    const int m0r = __builtin_amdgcn_readfirstlane(g.M0), mr = __builtin_amdgcn_readfirstlane(g.M);
+    const int m = l == 0 ? m0r : mr;
+    auto rfl_ptr = [](const uint32_t* p) {
+        const uint64_t v = (uint64_t)p;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+        return (const uint32_t*)(((uint64_t)hi << 32) | lo);
+    };
+    const uint32_t* adj0 = rfl_ptr(g.adj0);
+    const uint32_t* upper = rfl_ptr(g.upper);
+    const uint32_t* upper_off = rfl_ptr(g.upper_off);
+    w.vis.clear();
+    bool lossy = false;
+    if (lane == 0) {
+        bool unrec;
+        w.vis.insert(ep, unrec);
+    }
+    B.init(cand_key(dep, ep));
+    uint64_t* sk = reinterpret_cast<uint64_t*>(w.sd);  // sd + si: 64 x 8 B
+    wave_sync();
+    for (;;) {
+        const uint64_t t0 = VSG_CLK();
+        const uint64_t a = B.min_unexpanded();
+        if (a == VSG_KEY_EMPTY) break;
+        if (B.size > ef && B.count_below(a) >= ef) break;
+        B.mark_expanded(a);
+        const uint32_t na = (uint32_t)a & VSG_ID_MASK;
+        const uint32_t* row = l == 0 ? adj0 + (size_t)na * m0r : upper + ((size_t)upper_off[na] + (size_t)(l - 1)) * mr;
+        const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
+        ++nadj;
+        bool fresh = false, evicted = false;
+        if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
+        const uint64_t mask = __ballot(fresh);
+        lossy = lossy || __ballot(evicted) != 0;
+        const int cnt = popc64(mask);
+        if (fresh) w.todo[lanes_below(mask)] = nb;
+        wave_sync();
+        const uint64_t t1 = VSG_CLK();
+        pf.adj += t1 - t0;
+        if (cnt == 0) continue;
+        rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
+        wave_sync();
+        ndist += (uint64_t)cnt;
+        const uint64_t ck = lane < cnt ? cand_key(w.tdist[lane], w.todo[lane]) : VSG_KEY_EMPTY;
+        const uint64_t t2 = VSG_CLK();
+        pf.dist += t2 - t1;
+        admit<R>(B, lane < cnt, ck, lossy, ef, sk);
+        pf.merge += VSG_CLK() - t2;
+    }
+}
+
+
+// The top min(ef, |B|) keys of B in ascending order into w.list (buffer 0),
+// as the LDS-list beam leaves them (the heuristic selection walks it).  B is
+// consumed.
+template <int R>
+__device__ __forceinline__ void regset_to_list(RegSet<R>& B, int ef, WaveLds& w) {
+    const int lane = lane_id();
+    List& L = w.list;
+    const int lim = min(ef, B.size);
+    int x = 0;
+    for (; x < lim; ++x) {
+        uint64_t b = VSG_KEY_EMPTY;
+#pragma unroll
+        for (int r = 0; r < R; ++r) b = B.k[r] < b ? B.k[r] : b;
+        b = wave_min64(b);
+        if (b == VSG_KEY_EMPTY) break;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (B.k[r] == b) B.k[r] = VSG_KEY_EMPTY;
+        if (lane == 0) {
+            L.d0[x] = key_dist(b);
+            L.i0[x] = (uint32_t)b & VSG_ID_MASK;
+        }
+    }
+    L.cur = 0;
+    L.size = x;
+    wave_sync();
+}
+
+
+}  // namespace vsg

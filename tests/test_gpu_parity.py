@@ -477,7 +477,7 @@ def test_hnsw_cooperative_search_bitexact(waves, monkeypatch):
         np.testing.assert_array_equal(a1.distances, a2.distances)
 
 
-@pytest.mark.parametrize("metric,dim,M", [("l2sq", 64, 16), ("ip", 32, 8)])
+@pytest.mark.parametrize("metric,dim,M", [("l2sq", 64, 16), ("ip", 32, 8), ("l2sq", 48, 32)])
 def test_hnsw_register_search_bitexact(metric, dim, M, monkeypatch):
     """Register-resident candidate set (hnsw_search_reg_kernel): bit-exact vs
     the oracle on integer data for every register-row class (ef 10..1024),

@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--config", type=int, default=1, help="seed set (BASELINE.json configs index)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--rerank-leg", type=int, default=1,
+                    help="N=1 f32 storage: also time the opt-in f16 traversal + f32 re-rank mode")
     ap.add_argument("--mode", default="hnsw", choices=("hnsw", "exact"),
                     help="exact: brute-force MFMA path (C5: --rows 1000000 --dim 1536 --metric ip)")
     ap.add_argument("--batch", type=int, default=1024, help="exact mode: queries per step")
@@ -184,11 +186,11 @@ def hnsw_leg(c, mode):
     def kshard(ef):
         return min(a.k, ef) if sharded else a.k
 
-    sweep = []
-    if a.ef:
-        ef = a.ef
-        sweep.append((ef, recall_of(search(qgt, ef, kshard(ef))[0])))
-    else:
+    def sweep_ef(fixed):
+        sweep = []
+        if fixed:
+            sweep.append((fixed, recall_of(search(qgt, fixed, kshard(fixed))[0])))
+            return fixed, sweep
         grid = (4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512, 768, 1024)
         if not sharded:
             grid = tuple(e for e in grid if e >= max(16, a.k))
@@ -215,6 +217,9 @@ def hnsw_leg(c, mode):
                 else:
                     e_lo = mid
             ef = e_hi
+        return ef, sweep
+
+    ef, sweep = sweep_ef(a.ef)
     recall = dict(sweep)[ef]
     ks = kshard(ef)
 
@@ -259,7 +264,42 @@ def hnsw_leg(c, mode):
         el2 = c.max_over_ranks(time.perf_counter() - t0)
         at_cfg = {"ef": e2, "k_shard": kshard(e2), "qps": round(queries_done / el2, 1),
                   "ms_per_step": round(1000.0 * el2 / a.steps, 3), "recall_at_10": round(r2, 4)}
+    # opt-in f16 traversal + exact f32 re-rank on the same graph (csrc/rerank.hip):
+    # reported beside the headline, never as `value` (the walk reads f16 rows)
+    rerank = None
+    if a.rerank_leg and not sharded and a.quant == "f32" and world == 1:
+        index.set_f16_traversal(True)
+        search(qgt[:1], 16, a.k)  # builds the f16 copy (untimed, once per index state)
+        ef_r, sw_r = sweep_ef(0)
+        for _ in range(max(1, a.warmup)):
+            search(q, ef_r, a.k)
+        index.reset_stats()
+        km = 0.0
+        c.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            ev0.record(c.stream)
+            index.search_device(q, a.k, ef_r, stream=c.stream)
+            ev1.record(c.stream)
+            torch.cuda.synchronize()
+            km += ev0.elapsed_time(ev1)
+        c.barrier()
+        el_r = c.max_over_ranks(time.perf_counter() - t0)
+        st_r = index.stats()
+        rb16 = ((a.dim + 7) // 8) * 16
+        ab_r = (st_r["search_distances"] * rb16 + st_r["search_adjacency"] * 2 * a.M * 4) / a.steps \
+            + a.queries * ef_r * row_bytes  # re-rank reads the beam's f32 rows
+        index.set_f16_traversal(False)
+        rerank = {"qps": round(queries_done / el_r, 1), "ms_per_step": round(1000.0 * el_r / a.steps, 3),
+                  "ef": ef_r, "recall_at_10": round(dict(sw_r)[ef_r], 4), "ef_sweep": sw_r,
+                  "kernels_ms": round(km / a.steps, 3),
+                  "alg_bytes_per_step": int(ab_r),
+                  "achieved_gbs": round(ab_r / (km / a.steps * 1e-3) / 1e9, 1),
+                  "dist_evals_per_query": round(st_r["search_distances"] / max(1, st_r["search_queries"]), 1),
+                  "note": "opt-in mode (no usearch equivalent): HNSW walk over an f16 copy of the rows, "
+                          "ef-beam re-ranked with exact f32 distances; same graph as the headline"}
     return {
+        "f16_rerank": rerank,
         "mode": mode, "index": index, "q": q, "x": x, "nloc": nloc,
         "qps": queries_done / elapsed, "ms_per_step": 1000.0 * elapsed / a.steps,
         "ef": ef, "k_shard": ks, "recall": recall, "sweep": sweep,
@@ -312,7 +352,8 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(head["ms_per_step"], 3),
         "higher_is_better": True,
-        "scaling": "weak" if replica else "strong",
+        # N=1 is the first point of the replica series the default N>1 run reports
+        "scaling": "weak" if (replica or (world == 1 and a.multi != "shard")) else "strong",
         "vs_baseline": None,
         "dtype": a.quant,
         "data": f"synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py), "
@@ -343,6 +384,7 @@ def main():
                            "frac": round(head["build_alg_bytes"] / head["build_s"] / 1e9 / HBM_PEAK_GBS, 4),
                            "alg_bytes": int(head["build_alg_bytes"])},
         "at_config_ef": head["at_config_ef"],
+        "f16_traversal_rerank": head.get("f16_rerank"),
     }
     if "shard" in res and head["mode"] != "shard":
         s = res["shard"]

@@ -50,6 +50,11 @@ extern "C" {
 /* flags: store vectors only (no HNSW graph); exact_search works, search returns
  * VSG_EUNSUPPORTED.  The brute-force MFMA configuration. */
 #define VSG_FLAG_EXACT_ONLY 1u
+/* flags: HNSW search walks an f16 copy of the (f32) rows and re-ranks its beam
+ * of ef candidates with exact f32 distances (rerank.hip).  Returned distances
+ * are the f32 metric values; the candidate set can differ from an f32 walk.
+ * No usearch equivalent (opt-in; f32 storage only). */
+#define VSG_FLAG_F16_TRAVERSAL 2u
 
 typedef struct vsg_index vsg_index_t;
 
@@ -123,6 +128,11 @@ int vsg_index_search(vsg_index_t* index, const float* queries, size_t nq, size_t
  * same signature; ties broken by insertion slot. */
 int vsg_index_exact_search(vsg_index_t* index, const float* queries, size_t nq, size_t k,
                            uint64_t* out_keys, float* out_distances, size_t* out_counts);
+
+/* Switch the f16 traversal + f32 re-rank mode (VSG_FLAG_F16_TRAVERSAL) on an
+ * existing index; the f16 copy is built by the next search (and freed when
+ * switched off).  VSG_EINVAL unless the storage is f32.  Not in usearch. */
+int vsg_index_set_f16_traversal(vsg_index_t* index, int enable);
 
 /* Device-resident variants: queries (f32 nq x dimensions), outputs and counts
  * (u32, optional) in device memory; enqueued on `stream` (NULL => the HIP

@@ -210,7 +210,7 @@ __global__ __launch_bounds__(64) void hnsw_search_kernel(SearchParams p) {
             const uint64_t m = __ballot(alive);
             const int pos = count + lanes_below(m);
             if (alive && pos < p.k) {
-                ok[pos] = p.keys[id];
+                ok[pos] = p.keys ? p.keys[id] : (uint64_t)id;
                 od[pos] = L.D()[i];
             }
             count += popc64(m);
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(64 * NW) void hnsw_search_wg_kernel(SearchParams p)
                 const uint64_t m = __ballot(alive);
                 const int pos = count + lanes_below(m);
                 if (alive && pos < p.k) {
-                    ok[pos] = p.keys[id];
+                    ok[pos] = p.keys ? p.keys[id] : (uint64_t)id;
                     od[pos] = L.D()[i];
                 }
                 count += popc64(m);

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(64) void hnsw_search_reg_kernel(SearchParams p) {
             }
         }
         wave_sync();
-        for (int j = lane; j < count; j += 64) ok[j] = p.keys[sel[j]];
+        for (int j = lane; j < count; j += 64) ok[j] = p.keys ? p.keys[sel[j]] : (uint64_t)sel[j];
     }
     for (int j = count + lane; j < p.k; j += 64) {
         ok[j] = ~0ull;

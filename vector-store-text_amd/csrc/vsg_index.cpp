@@ -151,6 +151,15 @@ struct vsg_index {
     uint64_t* d_keys = nullptr;
     uint8_t* d_flags = nullptr;
     float* d_sqnorm = nullptr;  // |stored row|^2 (MFMA exact L2 expansion)
+    uint64_t vec_gen = 0;       // bumped when rows are rewritten or moved (shadow invalidation)
+
+    // f16 traversal copy (vsg_index_set_f16_traversal; rerank.hip): built lazily by
+    // the first search after rows change, rows [0, shadow_rows) current for shadow_gen
+    bool f16_trav = false;
+    std::mutex shadow_mu;
+    uint8_t* d_vecs16 = nullptr;
+    size_t shadow_cap = 0, shadow_rows = 0, row_bytes16 = 0;
+    uint64_t shadow_gen = ~0ull;
     unsigned long long* d_stats = nullptr;  // [0..2] search, [3..4] build
 
     std::vector<int8_t> h_levels;
@@ -201,6 +210,7 @@ static void free_dev(vsg_index* h) {
     h->ws_free.clear();
     hipFree(h->d_rm);
     hipFree(h->d_vecs);
+    hipFree(h->d_vecs16);
     hipFree(h->d_adj0);
     hipFree(h->d_upper_off);
     hipFree(h->d_upper);
@@ -242,6 +252,7 @@ static int reserve_locked(vsg_index* h, size_t capacity) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     hipFree(h->d_vecs);
     h->d_vecs = nv;
+    h->vec_gen++;
     int rc;
     if ((rc = grow_array(&h->d_adj0, s * h->M0, capacity * h->M0, 0xFF, h->stream))) return rc;
     if ((rc = grow_array(&h->d_upper_off, s, capacity, 0xFF, h->stream))) return rc;
@@ -497,6 +508,12 @@ int vsg_index_new(const vsg_index_options_t* o, vsg_index_t** out) {
     h->ef = o->expansion_search ? (int)o->expansion_search : 64;
     if (h->efc > 1024) h->efc = 1024;
     h->elem = h->st == ST_F16 ? 2 : 4;
+    h->f16_trav = (o->flags & VSG_FLAG_F16_TRAVERSAL) != 0;
+    if (h->f16_trav && h->st != ST_F32) {
+        delete h;
+        return fail(VSG_EINVAL, "VSG_FLAG_F16_TRAVERSAL needs f32 storage");
+    }
+    h->row_bytes16 = (size_t)(h->dim + 7) / 8 * 16;
     const size_t per_chunk = 16 / h->elem;
     const size_t padded = (h->dim + per_chunk - 1) / per_chunk * per_chunk;
     h->row_bytes = padded * h->elem;
@@ -703,6 +720,30 @@ static void ws_release(vsg_index* h, Workspace* w, hipStream_t s) {
     h->ws_free.push_back(w);
 }
 
+// Bring the f16 traversal copy up to date (caller holds h->mu shared): rows are
+// append-only between vec_gen bumps, so only [shadow_rows, slots) is converted.
+static int ensure_shadow(vsg_index* h, hipStream_t s) {
+    std::lock_guard<std::mutex> g(h->shadow_mu);
+    if (h->shadow_gen != h->vec_gen || h->shadow_cap < h->slots) {
+        if (h->shadow_cap < h->cap) {
+            hipFree(h->d_vecs16);
+            h->d_vecs16 = nullptr;
+            h->shadow_cap = 0;
+            HIP_TRY(dev_alloc(&h->d_vecs16, h->cap * h->row_bytes16));
+            h->shadow_cap = h->cap;
+        }
+        h->shadow_rows = 0;
+        h->shadow_gen = h->vec_gen;
+    }
+    if (h->shadow_rows < h->slots) {
+        HIP_TRY(launch_shadow_f16(h->d_vecs, h->row_bytes, h->shadow_rows, h->slots, h->dim, h->d_vecs16,
+                                  h->row_bytes16, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        h->shadow_rows = h->slots;
+    }
+    return VSG_OK;
+}
+
 static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, size_t k, size_t ef,
                                 uint64_t* ok, float* od, uint32_t* oc, hipStream_t s, bool exact) {
     if (k == 0) return fail(VSG_EINVAL, "k must be >= 1 (Limit is NonZeroUsize)");
@@ -734,11 +775,27 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         if (slots == 0) nblocks = 1;
         np = nq * (size_t)nblocks * k;
     }
+    // f16 traversal: the beam (ef slots) of the f16 search is re-ranked in f32
+    const bool rerank = !exact && h->f16_trav && h->slots > 0;
+    size_t efr = ef ? ef : (size_t)h->ef;
+    efr = std::min<size_t>(std::max(efr, k), 1024);
+    size_t rr_b = 0;
+    if (rerank) {
+        int rc0 = ensure_shadow(h, s);
+        if (rc0) return rc0;
+        // f16 queries | candidate slots | candidate distances | candidate counts
+        rr_b = align256(nq * h->row_bytes16) + align256(nq * efr * 8) + 2 * align256(nq * efr * 4);
+    }
     const size_t qp_b = align256(nq * h->row_bytes), qsq_b = use_mfma ? align256(nq * 4) : 0,
                  part_b = align256(np * 4);
     Workspace* ws = nullptr;
-    int rc = ws_acquire(h, qp_b + qsq_b + 2 * part_b, s, &ws);
+    int rc = ws_acquire(h, qp_b + qsq_b + 2 * part_b + rr_b, s, &ws);
     if (rc) return rc;
+    uint8_t* rr = ws->base + qp_b + qsq_b + 2 * part_b;
+    uint8_t* q16 = rr;
+    uint64_t* ck = reinterpret_cast<uint64_t*>(q16 + align256(nq * h->row_bytes16));
+    float* cd = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ck) + align256(nq * efr * 8));
+    uint32_t* cc = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(cd) + align256(nq * efr * 4));
     uint8_t* qp = ws->base;
     float* qsq = use_mfma ? reinterpret_cast<float*>(ws->base + qp_b) : nullptr;
     float* pd = reinterpret_cast<float*>(ws->base + qp_b + qsq_b);
@@ -811,7 +868,38 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         // +12-46% at ef >= 192, profiles/r01_search_phases.jsonl);
         // VSG_SEARCH_REG=0 selects the LDS-list kernels
         p.reg = env_double("VSG_SEARCH_REG", 1) != 0 ? 1 : 0;
-        err = launch_search(h->st, h->mk, p, s);
+        if (!rerank) {
+            err = launch_search(h->st, h->mk, p, s);
+        } else {
+            err = launch_prepare(ST_F16, q_dev, nq, h->dim, h->normalize, q16, h->row_bytes16, s);
+            p.g.vecs = h->d_vecs16;
+            p.g.row_bytes = h->row_bytes16;
+            p.g.nchunks = (int)(h->row_bytes16 / 16);
+            p.queries = q16;
+            p.k = (int)e;  // the whole beam goes to the re-rank
+            p.keys = nullptr;
+            p.out_keys = ck;
+            p.out_dist = cd;
+            p.out_counts = cc;
+            if (err == hipSuccess) err = launch_search(ST_F16, h->mk, p, s);
+            if (err == hipSuccess) {
+                RerankParams rp{};
+                rp.vecs = h->d_vecs;
+                rp.row_bytes = h->row_bytes;
+                rp.nchunks = h->nchunks;
+                rp.queries = qp;
+                rp.cand = ck;
+                rp.cand_counts = cc;
+                rp.nq = (int)nq;
+                rp.kc = (int)e;
+                rp.k = (int)k;
+                rp.keys = h->d_keys;
+                rp.out_keys = ok;
+                rp.out_dist = od;
+                rp.out_counts = oc;
+                err = launch_rerank(h->mk, rp, s);
+            }
+        }
     } else if (err == hipSuccess) {
         ExactParams ep{};
         ep.vecs = h->d_vecs;
@@ -951,6 +1039,25 @@ int vsg_index_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, 
     return search_host(h, queries, nq, k, ef, out_keys, out_distances, out_counts, false);
 }
 
+int vsg_index_set_f16_traversal(vsg_index_t* h, int enable) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    if (enable && h->st != ST_F32) return fail(VSG_EINVAL, "f16 traversal needs f32 storage");
+    if (enable && (h->opt.flags & VSG_FLAG_EXACT_ONLY)) return fail(VSG_EUNSUPPORTED, "exact-only index");
+    DeviceGuard dg(h->device);
+    std::lock_guard<std::mutex> g(h->shadow_mu);
+    h->f16_trav = enable != 0;
+    h->opt.flags = enable ? (h->opt.flags | VSG_FLAG_F16_TRAVERSAL) : (h->opt.flags & ~VSG_FLAG_F16_TRAVERSAL);
+    if (!enable && h->d_vecs16) {
+        HIP_TRY(hipDeviceSynchronize());
+        hipFree(h->d_vecs16);
+        h->d_vecs16 = nullptr;
+        h->shadow_cap = h->shadow_rows = 0;
+        h->shadow_gen = ~0ull;
+    }
+    return VSG_OK;
+}
+
 int vsg_index_exact_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, uint64_t* out_keys,
                            float* out_distances, size_t* out_counts) {
     return search_host(h, queries, nq, k, 0, out_keys, out_distances, out_counts, true);
@@ -1075,6 +1182,7 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
     HIP_TRY(hipMalloc(&d, slots * h->dim * 4));
     HIP_TRY(hipMemcpyAsync(d, vectors, slots * h->dim * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(launch_prepare(h->st, d, slots, h->dim, h->normalize, h->d_vecs, h->row_bytes, st, h->d_sqnorm));
+    h->vec_gen++;
     HIP_TRY(hipMemcpyAsync(h->d_keys, keys, slots * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_flags, removed, slots, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_adj0, adj0, slots * h->M0 * 4, hipMemcpyHostToDevice, st));
@@ -1141,6 +1249,7 @@ int vsg_index_compact(vsg_index_t* h, size_t* n_dropped) {
         if (e == hipSuccess) e = launch_gather_rows(h->d_vecs, h->d_sqnorm, h->d_keys, d_idx, n, h->row_bytes, nv, nsq, nk, st);
         if (e == hipSuccess) e = hipMemcpyAsync(keys.data(), nk, n * 8, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipMemcpyAsync(h->d_vecs, nv, n * h->row_bytes, hipMemcpyDeviceToDevice, st);
+        h->vec_gen++;
         if (e == hipSuccess) e = hipMemcpyAsync(h->d_sqnorm, nsq, n * 4, hipMemcpyDeviceToDevice, st);
     }
     // drop the old graph

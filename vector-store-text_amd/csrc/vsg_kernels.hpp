@@ -26,7 +26,7 @@ struct SearchParams {
     uint32_t entry;
     int max_level;
     const uint8_t* flags;
-    const uint64_t* keys;
+    const uint64_t* keys;       // slot -> key (NULL: emit slots, f16-traversal candidates)
     uint64_t* out_keys;
     float* out_dist;
     uint32_t* out_counts;
@@ -103,6 +103,22 @@ struct MergeParams {
     uint32_t* out_counts;
 };
 
+// f16-traversal re-rank (rerank.hip): exact f32 distances of each query's
+// traversal candidates (slots from the f16 search), best k by (distance, slot)
+struct RerankParams {
+    const uint8_t* vecs;  // f32 image
+    size_t row_bytes;
+    int nchunks;
+    const uint8_t* queries;  // prepared f32 rows, row_bytes stride
+    const uint64_t* cand;    // nq x kc slots (~0 = none)
+    const uint32_t* cand_counts;
+    int nq, kc, k;
+    const uint64_t* keys;  // slot -> key
+    uint64_t* out_keys;
+    float* out_dist;
+    uint32_t* out_counts;
+};
+
 // key layout of the reverse-link pairs
 constexpr int PAIR_U_BITS = 29;
 constexpr int PAIR_V_SHIFT = 29;
@@ -122,6 +138,10 @@ hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipSt
 hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s);
 hipError_t launch_exact(Storage st, MetricKind mk, const ExactParams& p, hipStream_t s);
 hipError_t launch_merge_parts(const MergeParams& p, hipStream_t s);
+hipError_t launch_rerank(MetricKind mk, const RerankParams& p, hipStream_t s);
+// f32 image rows [r0, r1) -> f16 traversal copy (row_bytes16 stride, padding zeroed)
+hipError_t launch_shadow_f16(const uint8_t* vecs, size_t row_bytes, size_t r0, size_t r1, int dim,
+                             uint8_t* out, size_t row_bytes16, hipStream_t s);
 // returns hipErrorNotSupported when the MFMA path does not apply (k > 32)
 hipError_t launch_mfma_exact(MetricKind mk, const MfmaExactParams& p, hipStream_t s);
 constexpr int MFMA_BQ = 128, MFMA_BR = 128;

@@ -143,6 +143,7 @@ def lib() -> C.CDLL:
         "vsg_merge_topk_device": (C.c_int, [P, P, sz, sz, sz, sz, P, P, P]),
         "vsg_index_stats": (C.c_int, [P, C.POINTER(Stats)]),
         "vsg_index_reset_stats": (C.c_int, [P]),
+        "vsg_index_set_f16_traversal": (C.c_int, [P, C.c_int]),
         "vsg_index_graph_info": (C.c_int, [P, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz),
                                            C.POINTER(u32), C.POINTER(C.c_int)]),
         "vsg_index_export": (C.c_int, [P] * 8),

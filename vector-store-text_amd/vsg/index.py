@@ -50,12 +50,14 @@ class Matches:
 class Index:
     def __init__(self, dimensions: int, metric: str = "l2sq", quantization: str = "f32",
                  connectivity: int = 0, expansion_add: int = 0, expansion_search: int = 0,
-                 device: int = 0, seed: int = 0, exact_only: bool = False):
+                 device: int = 0, seed: int = 0, exact_only: bool = False,
+                 f16_traversal: bool = False):
         self.dimensions = int(dimensions)
         self.metric = metric
         self.quantization = quantization
         opt = Options(self.dimensions, METRICS[metric], SCALARS[quantization], connectivity,
-                      expansion_add, expansion_search, device, 1 if exact_only else 0, seed)
+                      expansion_add, expansion_search, device,
+                      (1 if exact_only else 0) | (2 if f16_traversal else 0), seed)
         h = C.c_void_p()
         check(lib().vsg_index_new(C.byref(opt), C.byref(h)))
         self._h = h
@@ -150,6 +152,11 @@ class Index:
         s = Stats()
         check(lib().vsg_index_stats(self._h, C.byref(s)))
         return {f: getattr(s, f) for f, _ in Stats._fields_}
+
+    def set_f16_traversal(self, enable: bool) -> None:
+        """Opt-in: HNSW search walks an f16 copy of the rows and re-ranks its ef-beam
+        with exact f32 distances (csrc/rerank.hip; no usearch equivalent)."""
+        check(lib().vsg_index_set_f16_traversal(self._h, 1 if enable else 0))
 
     def reset_stats(self) -> None:
         check(lib().vsg_index_reset_stats(self._h))

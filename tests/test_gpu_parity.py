@@ -185,15 +185,16 @@ def test_reference_integration_kat(metric):
 # ------------------------------------------------------------------- HNSW --
 
 @pytest.mark.parametrize("reg", ["1", "0"])
-@pytest.mark.parametrize("metric,dim,M", [("l2sq", 32, 8), ("l2sq", 128, 16), ("ip", 64, 16)])
+@pytest.mark.parametrize("metric,dim,M", [("l2sq", 32, 8), ("l2sq", 128, 16), ("ip", 64, 16), ("l2sq", 384, 16)])
 def test_hnsw_search_same_graph_bitexact(metric, dim, M, reg, monkeypatch):
     """Oracle-built graph imported into HBM: GPU traversal == oracle traversal
     (integer data => exact distances => identical visiting order), for the
     register-set kernel (default) and the LDS-list kernel."""
     monkeypatch.setenv("VSG_SEARCH_REG", reg)
     n = 6000
-    x = G.uint8_valued(n, dim, 31) / (16.0 if metric == "ip" else 1.0)
-    q = G.uint8_valued(100, dim, 32) / (16.0 if metric == "ip" else 1.0)
+    div = 16.0 if metric == "ip" else (4.0 if dim > 256 else 1.0)  # keep sums < 2^24 (exact)
+    x = np.floor(G.uint8_valued(n, dim, 31) / div)
+    q = np.floor(G.uint8_valued(100, dim, 32) / div)
     h = O.HnswOracle(dim, metric, M, 64, 48, seed=5)
     h.add(np.arange(n), x.astype(np.float32))
     h.remove(np.arange(0, n, 17))
@@ -238,7 +239,8 @@ def test_hnsw_forgetful_visited_table_is_exact(monkeypatch):
 
 
 @pytest.mark.parametrize("metric,dim,quant", [("l2sq", 64, "f32"), ("cos", 128, "f32"),
-                                              ("ip", 96, "f32"), ("l2sq", 64, "f16")])
+                                              ("ip", 96, "f32"), ("l2sq", 64, "f16"),
+                                              ("cos", 384, "f32"), ("cos", 768, "f16")])
 def test_hnsw_gpu_build_recall_vs_oracle(metric, dim, quant):
     n, nq = 20000, 300
     bs, qs, ms = G.config_seeds(1)
@@ -548,3 +550,33 @@ def test_full_size_c2_kernels_agree(monkeypatch):
     k48 = idx.search_device(q, 10, 48)[0].cpu().numpy()
     assert recall(k48, gt, 10) >= 0.95
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("metric,dim,quant", [("l2sq", 384, "f32"), ("ip", 320, "f32"),
+                                              ("l2sq", 768, "f16"), ("ip", 520, "f16")])
+def test_shape96_rows_bitexact(metric, dim, quant, monkeypatch):
+    """Rows of 65..96 16-B chunks use the two-rows-per-wave shape (G=32, VM=3):
+    exact search and HNSW traversal of an oracle-built graph stay bit-exact on
+    integer data (values <= 15, so every f32 partial sum is exact)."""
+    n = 5000
+    x = np.floor(G.uint8_valued(n, dim, 91) / 16.0)
+    q = np.floor(G.uint8_valued(80, dim, 92) / 16.0)
+    ok, od, _ = O.exact_search(metric, x, q, 10)
+    h = O.HnswOracle(dim, metric, 16, 64, 48, seed=6)
+    h.add(np.arange(n), x.astype(np.float32))
+    h.remove(np.arange(0, n, 11))
+    idx = vsg.Index(dim, metric, quant, 16, 64, 48, seed=6)
+    idx.import_graph(h.export())
+    ex = vsg.Index(dim, metric, quant, exact_only=True)
+    ex.add(np.arange(n), x)
+    for mfma in ("1", "0"):  # f32: MFMA tile kernel and the VALU kernel (shape-dispatched)
+        monkeypatch.setenv("VSG_EXACT_MFMA", mfma)
+        m = ex.exact_search(q, 10)
+        np.testing.assert_array_equal(m.keys, ok)
+        np.testing.assert_array_equal(m.distances, od)
+    for ef in (10, 64, 300):
+        hk, hd, hc = h.search(q, 10, ef)
+        m = idx.search(q, 10, ef)
+        np.testing.assert_array_equal(m.counts, hc)
+        np.testing.assert_array_equal(m.keys, hk)
+        np.testing.assert_array_equal(m.distances, hd)

@@ -7,6 +7,7 @@
 //   chunks <=  16: G 16, VM 1,  U 4
 //   chunks <=  32: G 32, VM 1,  U 8   (D=128 f32, D=256 f16)
 //   chunks <=  64: G 64, VM 1,  U 8
+//   chunks <=  96: G 32, VM 3,  U 4   (D=384 f32, D=768 f16)
 //   chunks <= 128: G 64, VM 2,  U 4
 //   chunks <= 192: G 64, VM 3,  U 4   (D=768 f32)
 //   chunks <= 256: G 64, VM 4,  U 2
@@ -18,6 +19,13 @@
 #include "vsg_kernels.hpp"
 
 namespace vsg {
+
+// 65..96 chunks (D=384 f32, D=768 f16): two 32-lane rows with 3 chunks per lane
+// instead of one 64-lane row whose second chunk is idle on a quarter of the lanes.
+// Measured on the f16 walk of C2: U=4 +13 %, U=2 +10 % (profiles/r01_shape96_probe.jsonl)
+#ifndef VSG_SHAPE96_U
+#define VSG_SHAPE96_U 4
+#endif
 
 template <int G_, int VM_, int U_> struct Shape {
     static constexpr int G = G_, VM = VM_, U = U_;
@@ -35,6 +43,9 @@ inline void dispatch_shape(int nc, F&& f) {
     else if (nc <= 16) f(Shape<16, 1, 4>{});
     else if (nc <= 32) f(Shape<32, 1, 8>{});
     else if (nc <= 64) f(Shape<64, 1, 8>{});
+#if VSG_SHAPE96_U
+    else if (nc <= 96) f(Shape<32, 3, VSG_SHAPE96_U>{});
+#endif
     else if (nc <= 128) f(Shape<64, 2, 4>{});
     else if (nc <= 192) f(Shape<64, 3, 4>{});
     else if (nc <= 256) f(Shape<64, 4, 2>{});

@@ -9,7 +9,8 @@
 //   chunks <=  64: G 64, VM 1,  U 8
 //   chunks <=  96: G 32, VM 3,  U 4   (D=384 f32, D=768 f16)
 //   chunks <= 128: G 64, VM 2,  U 4
-//   chunks <= 192: G 64, VM 3,  U 4   (D=768 f32)
+//   chunks <= 192: G 32, VM 6,  U 2   (D=768 f32; was G 64 VM 3 U 4: search +1.7 %, build +6 %,
+//                                      profiles/r01_shape192_probe.jsonl)
 //   chunks <= 256: G 64, VM 4,  U 2
 //   chunks <= 384: G 64, VM 6,  U 2   (D=1536 f32)
 //   chunks <= 512: G 64, VM 8,  U 2
@@ -47,7 +48,11 @@ inline void dispatch_shape(int nc, F&& f) {
     else if (nc <= 96) f(Shape<32, 3, VSG_SHAPE96_U>{});
 #endif
     else if (nc <= 128) f(Shape<64, 2, 4>{});
-    else if (nc <= 192) f(Shape<64, 3, 4>{});
+#ifdef VSG_SHAPE192
+    else if (nc <= 192) f(Shape<VSG_SHAPE192>{});  // probe builds only
+#else
+    else if (nc <= 192) f(Shape<32, 6, 2>{});
+#endif
     else if (nc <= 256) f(Shape<64, 4, 2>{});
     else if (nc <= 384) f(Shape<64, 6, 2>{});
     else if (nc <= 512) f(Shape<64, 8, 2>{});

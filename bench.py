@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--config", type=int, default=1, help="seed set (BASELINE.json configs index)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--upper-ef", type=int, default=8,
+                    help="N=1: also time the opt-in multi-entry descent at this level-1 beam width (0 = off)")
     ap.add_argument("--rerank-leg", type=int, default=1,
                     help="N=1 f32 storage: also time the opt-in f16 traversal + f32 re-rank mode")
     ap.add_argument("--mode", default="hnsw", choices=("hnsw", "exact"),
@@ -298,7 +300,33 @@ def hnsw_leg(c, mode):
                   "dist_evals_per_query": round(st_r["search_distances"] / max(1, st_r["search_queries"]), 1),
                   "note": "opt-in mode (no usearch equivalent): HNSW walk over an f16 copy of the rows, "
                           "ef-beam re-ranked with exact f32 distances; same graph as the headline"}
+    # opt-in multi-entry descent (level-1 beam of width upper_ef seeds level 0):
+    # same graph, f32 walk, then also with the f16 walk + re-rank; beside the headline
+    multi = None
+    if a.upper_ef > 1 and not sharded and world == 1:
+        multi = {"upper_ef": a.upper_ef,
+                 "note": "opt-in mode (not usearch's greedy descent): level-1 beam seeds the level-0 beam"}
+        index.set_upper_ef(a.upper_ef)
+        for tag, f16 in (("f32_walk", False), ("f16_walk_f32_rerank", True)):
+            if f16 and a.quant != "f32":
+                continue
+            index.set_f16_traversal(f16)
+            ef_m, sw_m = sweep_ef(0)
+            for _ in range(max(1, a.warmup)):
+                search(q, ef_m, a.k)
+            c.barrier()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                search(q, ef_m, a.k)
+                torch.cuda.synchronize()
+            c.barrier()
+            el_m = c.max_over_ranks(time.perf_counter() - t0)
+            multi[tag] = {"qps": round(queries_done / el_m, 1), "ms_per_step": round(1000.0 * el_m / a.steps, 3),
+                          "ef": ef_m, "recall_at_10": round(dict(sw_m)[ef_m], 4)}
+        index.set_f16_traversal(False)
+        index.set_upper_ef(0)
     return {
+        "multi_entry": multi,
         "f16_rerank": rerank,
         "mode": mode, "index": index, "q": q, "x": x, "nloc": nloc,
         "qps": queries_done / elapsed, "ms_per_step": 1000.0 * elapsed / a.steps,
@@ -385,6 +413,7 @@ def main():
                            "alg_bytes": int(head["build_alg_bytes"])},
         "at_config_ef": head["at_config_ef"],
         "f16_traversal_rerank": head.get("f16_rerank"),
+        "multi_entry": head.get("multi_entry"),
     }
     if "shard" in res and head["mode"] != "shard":
         s = res["shard"]

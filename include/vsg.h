@@ -134,6 +134,13 @@ int vsg_index_exact_search(vsg_index_t* index, const float* queries, size_t nq, 
  * switched off).  VSG_EINVAL unless the storage is f32.  Not in usearch. */
 int vsg_index_set_f16_traversal(vsg_index_t* index, int enable);
 
+/* Opt-in multi-entry descent (not usearch): upper_ef > 1 replaces the greedy
+ * step on level 1 by a beam of width min(upper_ef, ef) whose whole result set
+ * seeds the level-0 beam (register search kernel).  0 or 1 = usearch's greedy
+ * descent (default).  Raises recall at a given ef; results are no longer the
+ * usearch traversal's, so parity is by recall, not bit-exact. */
+int vsg_index_set_upper_ef(vsg_index_t* index, size_t upper_ef);
+
 /* Device-resident variants: queries (f32 nq x dimensions), outputs and counts
  * (u32, optional) in device memory; enqueued on `stream` (NULL => the HIP
  * default stream) and NOT synchronised.  Used by bench.py and the multi-GPU

@@ -567,7 +567,7 @@ bool shape_supported(int nchunks) { return nchunks >= 1 && nchunks <= 1024; }
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s) {
     if (p.nq <= 0) return hipSuccess;
-    if (p.reg) return launch_search_reg(st, mk, p, s);
+    if (p.reg || p.upper_ef > 1) return launch_search_reg(st, mk, p, s);  // multi-entry: reg kernel only
     const int nw = p.waves == 2 || p.waves == 4 ? p.waves : 1;
     const size_t lds = search_lds_bytes(p.ef, p.hash_size, nw);
     hipError_t err = hipSuccess;

@@ -223,12 +223,26 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
     const uint32_t* upper = rfl_ptr(g.upper);
     const uint32_t* upper_off = rfl_ptr(g.upper_off);
     w.vis.clear();
-    bool lossy = false;
-    if (lane == 0) {
-        bool unrec;
-        w.vis.insert(ep, unrec);
+    if (ep != VSG_EMPTY) {
+        if (lane == 0) {
+            bool unrec;
+            w.vis.insert(ep, unrec);
+        }
+        B.init(cand_key(dep, ep));
+    } else {
+        // seeded (beam_reg_seeded): B already holds the start set; mark it
+        // visited and unexpanded, admission bound open
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (B.k[r] != VSG_KEY_EMPTY) {
+                bool unrec;
+                w.vis.insert((uint32_t)B.k[r] & VSG_ID_MASK, unrec);
+            }
+        B.expm = 0;
+        B.tkey = VSG_KEY_EMPTY;
     }
-    B.init(cand_key(dep, ep));
+    bool lossy = false;
     uint64_t* sk = reinterpret_cast<uint64_t*>(w.sd);  // sd + si: 64 x 8 B
     wave_sync();
     for (;;) {

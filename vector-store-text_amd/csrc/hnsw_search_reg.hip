@@ -57,9 +57,18 @@ __global__ __launch_bounds__(64) void hnsw_search_reg_kernel(SearchParams p) {
         uint32_t cur = p.entry;
         float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
         ++ndist;
-        for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
         RegSet<R> B;
-        beam_reg<G, VM, U, T, MET, R>(g, q, 0, cur, dcur, p.ef, w, B, ndist, nadj, pf);
+        if (p.upper_ef > 1 && p.max_level >= 1) {
+            // opt-in multi-entry descent (not usearch): greedy down to level 2,
+            // an upper_ef-wide beam on level 1, and its whole result set seeds
+            // the level-0 beam
+            for (int l = p.max_level; l >= 2; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+            beam_reg<G, VM, U, T, MET, R>(g, q, 1, cur, dcur, min(p.upper_ef, p.ef), w, B, ndist, nadj, pf);
+            beam_reg<G, VM, U, T, MET, R>(g, q, 0, VSG_EMPTY, 0.f, p.ef, w, B, ndist, nadj, pf);
+        } else {
+            for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+            beam_reg<G, VM, U, T, MET, R>(g, q, 0, cur, dcur, p.ef, w, B, ndist, nadj, pf);
+        }
         // tombstones: skipped in the output, still traversed
         uint32_t alive = 0;
 #pragma unroll

@@ -156,6 +156,7 @@ struct vsg_index {
     // f16 traversal copy (vsg_index_set_f16_traversal; rerank.hip): built lazily by
     // the first search after rows change, rows [0, shadow_rows) current for shadow_gen
     bool f16_trav = false;
+    int upper_ef = 0;  // vsg_index_set_upper_ef: > 1 = multi-entry descent (opt-in)
     std::mutex shadow_mu;
     uint8_t* d_vecs16 = nullptr;
     size_t shadow_cap = 0, shadow_rows = 0, row_bytes16 = 0;
@@ -868,6 +869,7 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         // +12-46% at ef >= 192, profiles/r01_search_phases.jsonl);
         // VSG_SEARCH_REG=0 selects the LDS-list kernels
         p.reg = env_double("VSG_SEARCH_REG", 1) != 0 ? 1 : 0;
+        p.upper_ef = (int)env_double("VSG_SEARCH_UPPER_EF", h->upper_ef);
         if (!rerank) {
             err = launch_search(h->st, h->mk, p, s);
         } else {
@@ -1037,6 +1039,14 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
 int vsg_index_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
                      float* out_distances, size_t* out_counts) {
     return search_host(h, queries, nq, k, ef, out_keys, out_distances, out_counts, false);
+}
+
+int vsg_index_set_upper_ef(vsg_index_t* h, size_t upper_ef) {
+    if (!h) return fail(VSG_EINVAL, "null index");
+    if (upper_ef > 1024) return fail(VSG_EINVAL, "upper_ef > 1024");
+    std::unique_lock<std::shared_mutex> lk(h->mu);
+    h->upper_ef = (int)upper_ef;
+    return VSG_OK;
 }
 
 int vsg_index_set_f16_traversal(vsg_index_t* h, int enable) {

@@ -35,6 +35,7 @@ struct SearchParams {
     int hash_size;              // visited-table entries (hash_size_for)
     int waves;                  // waves per query: 1 (hnsw_search_kernel), 2 or 4 (cooperative)
     int reg;                    // 1: hnsw_search_reg_kernel (candidate set in VGPRs; ignores waves)
+    int upper_ef;               // > 1: level-1 beam of this width seeds level 0 (reg kernel; opt-in)
 };
 
 struct InsertParams {

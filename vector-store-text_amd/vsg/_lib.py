@@ -144,6 +144,7 @@ def lib() -> C.CDLL:
         "vsg_index_stats": (C.c_int, [P, C.POINTER(Stats)]),
         "vsg_index_reset_stats": (C.c_int, [P]),
         "vsg_index_set_f16_traversal": (C.c_int, [P, C.c_int]),
+        "vsg_index_set_upper_ef": (C.c_int, [P, sz]),
         "vsg_index_graph_info": (C.c_int, [P, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz),
                                            C.POINTER(u32), C.POINTER(C.c_int)]),
         "vsg_index_export": (C.c_int, [P] * 8),

@@ -158,6 +158,11 @@ class Index:
         with exact f32 distances (csrc/rerank.hip; no usearch equivalent)."""
         check(lib().vsg_index_set_f16_traversal(self._h, 1 if enable else 0))
 
+    def set_upper_ef(self, upper_ef: int) -> None:
+        """Opt-in multi-entry descent: a level-1 beam of this width seeds level 0
+        (0/1 = usearch greedy descent, the default)."""
+        check(lib().vsg_index_set_upper_ef(self._h, int(upper_ef)))
+
     def reset_stats(self) -> None:
         check(lib().vsg_index_reset_stats(self._h))
 

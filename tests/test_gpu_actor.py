@@ -197,3 +197,28 @@ def test_actor_upsert_stream_compacts():
         kk, dd = a.ann(cur[k], 1)
         assert dd[0] == 0.0
     a.close()
+
+
+def test_actor_f16_traversal_answers_exact_distances():
+    """Actor built with the opt-in f16 walk + f32 re-rank (VSG_FLAG_F16_TRAVERSAL):
+    single-query answers carry the exact f32 distance of each returned key
+    (integer rows: bit-exact vs numpy), ascending, and find the true top-10
+    (recall vs the oracle's brute force; the coalesced batches make the graph
+    timing-dependent, so no bit-exact comparison with a second actor)."""
+    n, dim = 6000, 64
+    x = G.uint8_valued(n, dim, 97)
+    q = G.uint8_valued(64, dim, 98)
+    ok, _, _ = O.exact_search("l2sq", x, q, 10)
+    b = Actor(dim, "l2sq", connectivity=16, expansion_add=64, expansion_search=64, seed=8, f16_traversal=True)
+    for i in range(n):
+        b.add_or_replace(i, x[i])
+    b.flush()
+    hits = 0
+    for i in range(len(q)):
+        kb, db = b.ann(q[i], 10)
+        assert len(kb) == 10 and (np.diff(db) >= 0).all()
+        want = ((x[kb.astype(np.int64)].astype(np.float64) - q[i]) ** 2).sum(-1).astype(np.float32)
+        np.testing.assert_array_equal(db, want)
+        hits += len(set(kb.tolist()) & set(ok[i].tolist()))
+    assert hits / (10 * len(q)) >= 0.95
+    b.close()

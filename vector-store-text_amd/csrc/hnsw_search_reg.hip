@@ -62,8 +62,14 @@ __global__ __launch_bounds__(64) void hnsw_search_reg_kernel(SearchParams p) {
             // opt-in multi-entry descent (not usearch): greedy down to level 2,
             // an upper_ef-wide beam on level 1, and its whole result set seeds
             // the level-0 beam
+#ifdef VSG_UPPER_ALL_LEVELS
+            beam_reg<G, VM, U, T, MET, R>(g, q, p.max_level, cur, dcur, min(p.upper_ef, p.ef), w, B, ndist, nadj, pf);
+            for (int l = p.max_level - 1; l >= 1; --l)
+                beam_reg<G, VM, U, T, MET, R>(g, q, l, VSG_EMPTY, 0.f, min(p.upper_ef, p.ef), w, B, ndist, nadj, pf);
+#else
             for (int l = p.max_level; l >= 2; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
             beam_reg<G, VM, U, T, MET, R>(g, q, 1, cur, dcur, min(p.upper_ef, p.ef), w, B, ndist, nadj, pf);
+#endif
             beam_reg<G, VM, U, T, MET, R>(g, q, 0, VSG_EMPTY, 0.f, p.ef, w, B, ndist, nadj, pf);
         } else {
             for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);

@@ -41,7 +41,11 @@ template <int M_> struct MetTag {
 template <typename F>
 inline void dispatch_shape(int nc, F&& f) {
     if (nc <= 4) f(Shape<4, 1, 4>{});
+#ifdef VSG_SHAPE16
+    else if (nc <= 16) f(Shape<VSG_SHAPE16>{});  // probe builds only
+#else
     else if (nc <= 16) f(Shape<16, 1, 4>{});
+#endif
     else if (nc <= 32) f(Shape<32, 1, 8>{});
     else if (nc <= 64) f(Shape<64, 1, 8>{});
 #if VSG_SHAPE96_U

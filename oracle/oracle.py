@@ -44,6 +44,7 @@ def lib():
         L.orc_distance.restype = C.c_float
         L.orc_distance.argtypes = [C.c_int, P, P, sz]
         L.orc_set_fast_metric.argtypes = [C.c_int]
+        L.orc_fast_isa.restype = C.c_char_p
         L.orc_exact_search.argtypes = [C.c_int, P, P, P, sz, sz, P, sz, sz, P, P, P, C.c_int]
         L.orc_hnsw_new.restype = P
         L.orc_hnsw_new.argtypes = [sz, C.c_int, sz, sz, sz, C.c_uint64]
@@ -74,6 +75,10 @@ def sample_level(seed: int, slot: int, connectivity: int) -> int:
 
 def set_fast_metric(on: bool) -> None:
     lib().orc_set_fast_metric(1 if on else 0)
+
+
+def fast_isa() -> str:
+    return lib().orc_fast_isa().decode()
 
 
 def distance(metric: str, a, b) -> float:

@@ -48,65 +48,18 @@ int orc_sample_level(uint64_t seed, uint64_t slot, uint32_t connectivity) {
 
 /* --------------------------------------------------------------- metrics -- */
 
-/* CPU-baseline mode: SIMD multi-accumulator kernels (the shape of usearch's
- * SimSIMD back-end).  Parity mode (default): serial f32 loops exactly as the
+/* CPU-baseline mode: SIMD multi-accumulator kernels with FMA, dispatched to the
+ * host's widest ISA (the shape of usearch's SimSIMD back-end; vsg_fast.c).  Parity mode (default): serial f32 loops exactly as the
  * generic metric_*_gt.  The baseline switches to fast mode only for timing. */
 static int g_fast_metric = 0;
 void orc_set_fast_metric(int on) { g_fast_metric = on; }
 
-typedef float v8f __attribute__((vector_size(32)));
-
-static float hsum8(v8f v) {
-    float s = 0.f;
-    for (int i = 0; i < 8; ++i) s += v[i];
-    return s;
-}
-
-static float fast_distance(int metric, const float* a, const float* b, size_t dim) {
-    v8f s0 = {0}, s1 = {0}, n0 = {0}, n1 = {0}, m0 = {0}, m1 = {0};
-    size_t i = 0;
-    for (; i + 16 <= dim; i += 16) {
-        v8f a0, a1, b0, b1;
-        memcpy(&a0, a + i, 32);
-        memcpy(&a1, a + i + 8, 32);
-        memcpy(&b0, b + i, 32);
-        memcpy(&b1, b + i + 8, 32);
-        if (metric == ORC_METRIC_L2SQ) {
-            v8f d0 = a0 - b0, d1 = a1 - b1;
-            s0 += d0 * d0;
-            s1 += d1 * d1;
-        } else {
-            s0 += a0 * b0;
-            s1 += a1 * b1;
-            if (metric == ORC_METRIC_COS) {
-                n0 += a0 * a0;
-                n1 += a1 * a1;
-                m0 += b0 * b0;
-                m1 += b1 * b1;
-            }
-        }
-    }
-    float s = hsum8(s0 + s1), na = hsum8(n0 + n1), nb = hsum8(m0 + m1);
-    for (; i < dim; ++i) {
-        if (metric == ORC_METRIC_L2SQ) {
-            float d = a[i] - b[i];
-            s += d * d;
-        } else {
-            s += a[i] * b[i];
-            na += a[i] * a[i];
-            nb += b[i] * b[i];
-        }
-    }
-    if (metric == ORC_METRIC_L2SQ) return s;
-    if (metric == ORC_METRIC_IP) return 1.f - s;
-    if (na == 0.f && nb == 0.f) return 0.f;
-    if (na == 0.f || nb == 0.f) return 1.f;
-    return 1.f - s / (sqrtf(na) * sqrtf(nb));
-}
+/* host-ISA kernels (vsg_fast.c: AVX-512 + FMA when present, as SimSIMD dispatches) */
+float orc_fast_distance(int metric, const float* a, const float* b, size_t dim);
 
 /* usearch metric_l2sq_gt / metric_ip_gt / metric_cos_gt, f32 result type. */
 float orc_distance(int metric, const float* a, const float* b, size_t dim) {
-    if (g_fast_metric) return fast_distance(metric, a, b, dim);
+    if (g_fast_metric) return orc_fast_distance(metric, a, b, dim);
     if (metric == ORC_METRIC_L2SQ) {
         float s = 0.f;
         for (size_t i = 0; i < dim; ++i) {

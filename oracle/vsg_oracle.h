@@ -51,8 +51,11 @@ int orc_sample_level(uint64_t seed, uint64_t slot, uint32_t connectivity);
 
 /* usearch metric_*_gt restated: f32 serial accumulation. */
 float orc_distance(int metric, const float* a, const float* b, size_t dim);
-/* 1 => SIMD multi-accumulator metrics (CPU-baseline timing only). */
+/* 1 => SIMD multi-accumulator metrics with FMA at the host's widest ISA
+ * (CPU-baseline timing only; vsg_fast.c). */
 void orc_set_fast_metric(int on);
+/* ISA the fast metrics dispatch to: "avx512f+fma", "avx2+fma" or "scalar" */
+const char* orc_fast_isa(void);
 
 /* Exact top-k.  base: n x dim row-major, keys: n (NULL => key = row index),
  * removed: n flags or NULL.  Output rows of k, ascending (distance, key);

@@ -31,6 +31,16 @@ int main() {
         }
         if (m.size() != ref.size()) { std::printf("size mismatch\n"); return 1; }
     }
+    // reserved keys: after ordinary erasures left tombstones on
+    // the probe paths, UINT64_MAX-1 / UINT64_MAX are never found, erased or inserted
+    for (uint64_t rk : {vsg::KeyMap::DEAD, vsg::KeyMap::EMPTY}) {
+        const size_t before = m.size();
+        uint32_t v = 0;
+        if (m.find(rk, &v) || m.erase(rk, &v) || m.insert(rk, 1) || m.size() != before) {
+            std::printf("reserved key %llx accepted\n", (unsigned long long)rk);
+            return 1;
+        }
+    }
     std::printf("ok %zu\n", m.size());
     return 0;
 }

@@ -129,3 +129,68 @@ def test_load_rejects_damaged_payload(tmp_path):
     p.write_bytes(bytes(raw[:-8]))
     with pytest.raises(vsg.VsgError):
         vsg.Index.load(p)
+
+
+def test_load_validates_crafted_graph(tmp_path):
+    """A file whose checksums are valid but whose graph is not: adjacency
+    ids past the slot count, an entry point off the top level, upper rows outside
+    the table, a reserved live key -- each refused before any kernel reads it."""
+    from test_persistence_format import write_file
+    M, slots = 4, 6
+    chain = np.full((slots, 2 * M), 0xFFFFFFFF, np.uint32)
+    for s in range(slots):  # a ring on level 0
+        chain[s, 0], chain[s, 1] = (s + 1) % slots, (s - 1) % slots
+    ok = dict(dim=8, M=M, slots=slots, live=slots, upper_rows=0, entry=2, max_level=0, adj0=chain)
+    p = tmp_path / "g.vsg"
+    write_file(p, **ok)
+    b = vsg.Index.load(p)
+    assert b.size() == slots and int(b.search(np.zeros((1, 8), np.float32), 3).counts[0]) == 3
+    bad = chain.copy()
+    bad[3, 2] = slots + 5
+    cases = [(dict(ok, adj0=bad), "adjacency"),
+             (dict(ok, entry=slots), "entry"),
+             (dict(ok, max_level=2), "entry"),
+             (dict(ok, levels=[0, 0, 0, 1, 0, 0]), "level"),
+             (dict(ok, levels=[0, 0, 1, 0, 0, 0], max_level=1, upper_off=[0xFFFFFFFF, 0xFFFFFFFF, 0] + [0xFFFFFFFF] * 3),
+              "upper rows"),
+             (dict(ok, keys=[0, 1, 2, 2**64 - 2, 4, 5]), "reserved"),
+             (dict(ok, keys=[0, 1, 2, 3, 3, 5]), "duplicate")]
+    for kw, msg in cases:
+        write_file(p, **kw)
+        with pytest.raises(vsg.VsgError, match=msg):
+            vsg.Index.load(p)
+
+
+def test_import_validates_graph():
+    h = vsg.Index(8, "l2sq", connectivity=4)
+    n = 10
+    g = {"vectors": np.zeros((n, 8), np.float32), "keys": np.arange(n, dtype=np.uint64),
+         "removed": np.zeros(n, np.uint8), "levels": np.zeros(n, np.int8),
+         "adj0": np.full((n, 8), 0xFFFFFFFF, np.uint32), "upper_off": np.full(n, 0xFFFFFFFF, np.uint32),
+         "upper": np.zeros((0, 4), np.uint32), "entry": 0, "max_level": 0}
+    g["adj0"][1, 0] = 99
+    with pytest.raises(vsg.VsgError, match="adjacency"):
+        h.import_graph(g)
+    g["adj0"][1, 0] = 2
+    g["entry"] = 10
+    with pytest.raises(vsg.VsgError, match="entry"):
+        h.import_graph(g)
+    g["entry"] = 0
+    h.import_graph(g)
+    assert h.size() == n
+
+
+def test_reserved_keys_never_match():
+    """UINT64_MAX-1 is the key map's tombstone: removing or probing it after ordinary
+    removals must not hit a tombstone -- size stays right."""
+    idx = vsg.Index(4, "l2sq")
+    idx.add(np.arange(100), G.uint8_valued(100, 4, 2))
+    assert idx.remove(np.arange(0, 100, 3)) == 34
+    for _ in range(3):
+        assert idx.remove([2**64 - 2]) == 0
+        assert idx.remove([2**64 - 1]) == 0
+    assert not idx.contains(2**64 - 2) and idx.size() == 66
+    with pytest.raises(vsg.VsgError):
+        idx.add([2**64 - 2], np.zeros((1, 4), np.float32))
+    assert idx.remove([0, 1, 1, 2]) == 2  # 0 was removed before; 1 listed twice counts once
+    assert idx.size() == 64

@@ -210,6 +210,35 @@ def test_hnsw_search_same_graph_bitexact(metric, dim, M, reg, monkeypatch):
         np.testing.assert_array_equal(m.distances, od)
 
 
+def test_hnsw_same_graph_cos768_near_tie():
+    """768-d cosine, float data (the headline metric and shape):
+    the GPU stores unit rows and computes 1 - dot, the oracle (usearch metric_cos_gt)
+    computes 1 - ab/(|a||b|) per pair, so distances differ in the last bits.  On the
+    same graph (oracle-built -> HBM, and GPU-built -> oracle) both traversals return
+    equally good neighbours at every rank (|d_gpu - d_orc| <= 4e-6) and identical key
+    lists on >= 99 % of queries; a differing key is a swap among near-tied candidates."""
+    n, dim, nq = 20000, 768, 300
+    bs, qs, ms = G.config_seeds(1)
+    x = G.clustered(n, dim, bs + 7, ms)
+    q = G.clustered(nq, dim, qs + 7, ms)
+    h = O.HnswOracle(dim, "cos", 16, 128, 64, seed=11)
+    h.add(np.arange(n), x, threads=0)
+    h.remove(np.arange(0, n, 29))
+    idx = vsg.Index(dim, "cos", "f32", 16, 128, 64, seed=11)
+    idx.import_graph(h.export())
+    b = vsg.Index(dim, "cos", "f32", 16, 128, 64, seed=11)
+    b.add(np.arange(n), x)
+    hb = O.HnswOracle(dim, "cos", 16, 128, 64, seed=11)
+    hb.import_graph(b.export())
+    for gpu, orc in ((idx, h), (b, hb)):
+        for ef in (10, 64, 200):
+            ok, od, oc = orc.search(q, 10, ef)
+            m = gpu.search(q, 10, ef)
+            np.testing.assert_array_equal(m.counts, oc)
+            assert np.max(np.abs(m.distances - od)) <= 4e-6, (ef, float(np.max(np.abs(m.distances - od))))
+            assert np.all(m.keys == ok, axis=1).mean() >= 0.99
+
+
 def test_hnsw_forgetful_visited_table_is_exact(monkeypatch):
     """A visited table far smaller than the visited set (it forgets and the
     top-ef list de-duplicates) must not change results: bit-exact vs the

@@ -70,6 +70,25 @@ def test_rerank_tracks_appends_removals_and_compaction():
     _same(b.search(q, 16, 80), a.search(q, 16, 80))
 
 
+def test_rerank_after_compacting_everything():
+    """Every row removed, compaction drops all of them (slots -> 0), different rows
+    re-added: the f16 copy must be rebuilt, not reused."""
+    dim, nq = 32, 100
+    x = G.uint8_valued(8000, dim, 91)
+    q = G.uint8_valued(nq, dim, 92)
+    a = vsg.Index(dim, "l2sq", "f32", 16, 64, 40, seed=2)
+    b = vsg.Index(dim, "l2sq", "f32", 16, 64, 40, seed=2, f16_traversal=True)
+    for idx in (a, b):
+        idx.add(np.arange(4000), x[:4000])
+    _same(b.search(q, 10), a.search(q, 10))
+    for idx in (a, b):
+        assert idx.remove(np.arange(4000)) == 4000
+        assert idx.compact() == 4000
+        idx.add(np.arange(4000, 8000), x[4000:])
+    _same(b.search(q, 10, 64), a.search(q, 10, 64))
+    assert np.isin(b.search(q, 10).keys, np.arange(4000, 8000)).all()
+
+
 def test_rerank_requires_f32_storage():
     idx = vsg.Index(32, "l2sq", "f16")
     with pytest.raises(vsg.VsgError):

@@ -19,7 +19,9 @@ def fnv(data: bytes, h: int = 0xcbf29ce484222325) -> int:
 
 
 def write_file(path, dim=8, metric=2, quant=0, M=4, slots=5, live=4, upper_rows=2, payload_damage=False,
-               version=1):
+               version=1, entry=0, max_level=1, keys=None, levels=None, adj0=None, upper_off=None, upper=None):
+    """A checksum-valid index file from the documented layout; every section can be
+    overridden (crafted graphs for the load-time validation tests)."""
     row_bytes = ((dim * (4 if quant == 0 else 2) + 15) // 16) * 16
     opt = struct.pack("<6IiIQ", dim, metric, quant, M, 32, 16, 0, 0, 7)
     assert len(opt) == 40
@@ -29,16 +31,16 @@ def write_file(path, dim=8, metric=2, quant=0, M=4, slots=5, live=4, upper_rows=
     sections = [
         rng.standard_normal(slots * row_bytes // 4).astype(np.float32).tobytes(),  # rows
         np.ones(slots, np.float32).tobytes(),  # |x|^2
-        np.arange(slots, dtype=np.uint64).tobytes(),  # keys
+        (np.arange(slots, dtype=np.uint64) if keys is None else np.asarray(keys, np.uint64)).tobytes(),
         flags.tobytes(),
-        np.zeros(slots, np.int8).tobytes(),  # levels
-        np.full(slots * 2 * M, 0xFFFFFFFF, np.uint32).tobytes(),
-        np.full(slots, 0xFFFFFFFF, np.uint32).tobytes(),
-        np.zeros(upper_rows * M, np.uint32).tobytes(),
+        (np.zeros(slots, np.int8) if levels is None else np.asarray(levels, np.int8)).tobytes(),
+        (np.full(slots * 2 * M, 0xFFFFFFFF, np.uint32) if adj0 is None else np.asarray(adj0, np.uint32)).tobytes(),
+        (np.full(slots, 0xFFFFFFFF, np.uint32) if upper_off is None else np.asarray(upper_off, np.uint32)).tobytes(),
+        (np.zeros(upper_rows * M, np.uint32) if upper is None else np.asarray(upper, np.uint32)).tobytes(),
     ]
     payload = b"".join(sections)
     head = MAGIC + struct.pack("<II", version, 128) + opt + struct.pack(
-        "<4Q4IIiQ", slots, live, upper_rows, row_bytes, M, 2 * M, 32, 16, 0, 1, fnv(payload))
+        "<4Q4IIiQ", slots, live, upper_rows, row_bytes, M, 2 * M, 32, 16, entry, max_level, fnv(payload))
     head += struct.pack("<Q", fnv(head))
     assert len(head) == 128
     if payload_damage:

@@ -17,8 +17,10 @@ class KeyMap {
 
     size_t size() const { return live_; }
 
+    // reserved keys (EMPTY, DEAD) are never present: without this check a
+    // probe for DEAD would match the first tombstone on its path
     bool find(uint64_t k, uint32_t* v) const {
-        if (cap_ == 0) return false;
+        if (cap_ == 0 || k >= DEAD) return false;
         for (size_t i = hash(k) & (cap_ - 1);; i = (i + 1) & (cap_ - 1)) {
             if (keys_[i] == EMPTY) return false;
             if (keys_[i] == k) {
@@ -28,8 +30,9 @@ class KeyMap {
         }
     }
 
-    // false if k is already present (nothing changed)
+    // false if k is already present or reserved (nothing changed)
     bool insert(uint64_t k, uint32_t v) {
+        if (k >= DEAD) return false;
         if ((used_ + 1) * 2 > cap_) grow();
         size_t tomb = SIZE_MAX;
         for (size_t i = hash(k) & (cap_ - 1);; i = (i + 1) & (cap_ - 1)) {
@@ -47,7 +50,7 @@ class KeyMap {
     }
 
     bool erase(uint64_t k, uint32_t* v) {
-        if (cap_ == 0) return false;
+        if (cap_ == 0 || k >= DEAD) return false;
         for (size_t i = hash(k) & (cap_ - 1);; i = (i + 1) & (cap_ - 1)) {
             if (keys_[i] == EMPTY) return false;
             if (keys_[i] == k) {

@@ -478,6 +478,39 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
     return VSG_OK;
 }
 
+// Host-side consistency of a graph image handed in by import/load (a file that
+// passes its checksum may still be crafted): every adjacency id is a slot or
+// EMPTY, levels are in [0, 30], upper rows of each slot lie inside the upper
+// table, the entry point is a slot on the top level.  The search kernels index
+// HBM with these values, so nothing else guards them.
+static bool adj_ids_ok(const uint32_t* ids, size_t n, size_t slots) {
+    for (size_t i = 0; i < n; ++i)
+        if (ids[i] != 0xFFFFFFFFu && ids[i] >= slots) return false;
+    return true;
+}
+
+static int validate_graph(size_t slots, const int8_t* levels, const uint32_t* upper_off, size_t upper_rows,
+                          uint32_t entry, int max_level, bool exact_only) {
+    if (exact_only) {  // rows only: no entry point, levels unused by any kernel
+        if (entry != 0xFFFFFFFFu) return fail(VSG_EINVAL, "graph: entry point in an exact-only index");
+        return VSG_OK;
+    }
+    if (slots == 0) {
+        if (upper_rows || (entry != 0xFFFFFFFFu && max_level >= 0)) return fail(VSG_EINVAL, "graph: entry point in an empty graph");
+        return VSG_OK;
+    }
+    if (entry >= slots || max_level < 0 || max_level > 30 || levels[entry] != max_level)
+        return fail(VSG_EINVAL, "graph: entry point / max level inconsistent");
+    for (size_t i = 0; i < slots; ++i) {
+        const int L = levels[i];
+        if (L < 0 || L > max_level) return fail(VSG_EINVAL, "graph: level out of range at slot " + std::to_string(i));
+        if (L == 0) continue;
+        if (upper_off[i] == 0xFFFFFFFFu || (size_t)upper_off[i] + (size_t)L > upper_rows)
+            return fail(VSG_EINVAL, "graph: upper rows out of range at slot " + std::to_string(i));
+    }
+    return VSG_OK;
+}
+
 // ----------------------------------------------------------------- C ABI --
 
 extern "C" {
@@ -597,7 +630,20 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
     const uint32_t s0 = (uint32_t)h->slots;
     if ((rc = map_keys(h, keys, n, s0))) return rc;
     rc = add_rows(h, keys, vecs, n, device_src, user_stream, s0);
-    if (rc) unmap_keys(h, keys, n);
+    if (rc) {
+        // Roll back: the keys leave the map and live drops back.  Rows that
+        // already got slots stay as tombstones -- earlier batches of this call
+        // may be linked into the graph, so the slots cannot be handed out again.
+        const std::string msg = g_last_error;
+        unmap_keys(h, keys, n);
+        if (h->slots > s0) {
+            const size_t got = h->slots - s0;
+            (void)hipMemsetAsync(h->d_flags + s0, 1, got, h->stream);
+            (void)hipStreamSynchronize(h->stream);
+            h->live -= got;
+        }
+        g_last_error = msg;
+    }
     return rc;
 }
 
@@ -645,11 +691,15 @@ int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_r
     if (!h || (!keys && n)) return fail(VSG_EINVAL, "null argument");
     std::unique_lock<std::shared_mutex> lk(h->mu);
     DeviceGuard dg(h->device);
+    // tombstone on the device first; the keys leave the map only once that
+    // succeeded (a failed call changes nothing).  Duplicates in `keys` count once.
     std::vector<uint32_t> slots;
+    std::vector<uint64_t> hit;
     for (size_t i = 0; i < n; ++i) {
         uint32_t slot;
-        if (!h->keys.erase(keys[i], &slot)) continue;
+        if (!h->keys.find(keys[i], &slot)) continue;
         slots.push_back(slot);
+        hit.push_back(keys[i]);
     }
     if (!slots.empty()) {
         int rc = ensure_buf(&h->d_rm, h->rm_cap, slots.size());
@@ -658,7 +708,10 @@ int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_r
         HIP_TRY(launch_set_flags(h->d_flags, h->d_rm, slots.size(), 1, h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));
     }
-    h->live -= slots.size();
+    size_t removed = 0;
+    for (uint64_t k : hit) removed += h->keys.erase(k, nullptr) ? 1 : 0;
+    slots.resize(removed);
+    h->live -= removed;
     if (n_removed) *n_removed = slots.size();
     return VSG_OK;
 }
@@ -725,7 +778,7 @@ static void ws_release(vsg_index* h, Workspace* w, hipStream_t s) {
 // append-only between vec_gen bumps, so only [shadow_rows, slots) is converted.
 static int ensure_shadow(vsg_index* h, hipStream_t s) {
     std::lock_guard<std::mutex> g(h->shadow_mu);
-    if (h->shadow_gen != h->vec_gen || h->shadow_cap < h->slots) {
+    if (h->shadow_gen != h->vec_gen || h->shadow_cap < h->slots || h->shadow_rows > h->slots) {
         if (h->shadow_cap < h->cap) {
             hipFree(h->d_vecs16);
             h->d_vecs16 = nullptr;
@@ -960,10 +1013,10 @@ static void ctx_release(vsg_index* h, SearchCtx* c) {
 
 static int ctx_reserve(SearchCtx* c, size_t pin_bytes, size_t dev_bytes) {
     if (pin_bytes > c->pin_cap) {
+        const size_t want = std::max(pin_bytes, c->pin_cap * 2);  // before the old capacity is cleared
         if (c->pin) HIP_TRY(hipHostFree(c->pin));
         c->pin = nullptr;
         c->pin_cap = 0;
-        const size_t want = std::max(pin_bytes, c->pin_cap * 2);
         // coherent (snooped) pinned memory: the buffer is written and read by
         // the CPU around the DMA; a non-coherent mapping lets the copy engine
         // read lines still dirty in the CPU caches (seen as stale query rows)
@@ -971,10 +1024,10 @@ static int ctx_reserve(SearchCtx* c, size_t pin_bytes, size_t dev_bytes) {
         c->pin_cap = want;
     }
     if (dev_bytes > c->dev_cap) {
+        const size_t want = std::max(dev_bytes, c->dev_cap * 2);
         if (c->dev) HIP_TRY(hipFree(c->dev));
         c->dev = nullptr;
         c->dev_cap = 0;
-        const size_t want = std::max(dev_bytes, c->dev_cap * 2);
         HIP_TRY(hipMalloc((void**)&c->dev, want));
         c->dev_cap = want;
     }
@@ -1184,7 +1237,22 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
     DeviceGuard dg(h->device);
     if (h->slots) return fail(VSG_EINVAL, "import requires an empty index");
     if (slots == 0) return VSG_OK;
-    int rc = reserve_locked(h, slots);
+    if (slots > MAX_SLOTS) return fail(VSG_EINVAL, "import: more than 2^29 slots per shard");
+    if (!vectors || !keys || !removed || !levels || !adj0 || !upper_off || (upper_rows && !upper))
+        return fail(VSG_EINVAL, "null argument");
+    int rc = validate_graph(slots, levels, upper_off, upper_rows, entry, max_level,
+                            (h->opt.flags & VSG_FLAG_EXACT_ONLY) != 0);
+    if (rc) return rc;
+    if (!adj_ids_ok(adj0, slots * h->M0, slots) || !adj_ids_ok(upper, upper_rows * h->M, slots))
+        return fail(VSG_EINVAL, "import: adjacency id out of range");
+    {
+        KeyMap probe;
+        probe.reserve(slots);
+        for (size_t i = 0; i < slots; ++i)
+            if (!(removed[i] & 1) && !probe.insert(keys[i], (uint32_t)i))
+                return fail(VSG_EINVAL, "import: reserved or duplicate live key " + std::to_string(keys[i]));
+    }
+    rc = reserve_locked(h, slots);
     if (rc) return rc;
     if ((rc = ensure_upper(h, upper_rows))) return rc;
     hipStream_t st = h->stream;
@@ -1259,9 +1327,10 @@ int vsg_index_compact(vsg_index_t* h, size_t* n_dropped) {
         if (e == hipSuccess) e = launch_gather_rows(h->d_vecs, h->d_sqnorm, h->d_keys, d_idx, n, h->row_bytes, nv, nsq, nk, st);
         if (e == hipSuccess) e = hipMemcpyAsync(keys.data(), nk, n * 8, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipMemcpyAsync(h->d_vecs, nv, n * h->row_bytes, hipMemcpyDeviceToDevice, st);
-        h->vec_gen++;
         if (e == hipSuccess) e = hipMemcpyAsync(h->d_sqnorm, nsq, n * 4, hipMemcpyDeviceToDevice, st);
     }
+    // rows moved (or all dropped): the f16 traversal copy is stale either way
+    h->vec_gen++;
     // drop the old graph
     if (e == hipSuccess) e = hipMemsetAsync(h->d_adj0, 0xFF, s * h->M0 * 4, st);
     if (e == hipSuccess) e = hipMemsetAsync(h->d_upper_off, 0xFF, s * 4, st);
@@ -1483,6 +1552,7 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
     if ((rc = ensure_upper(h, fh.upper_rows))) return rc;
     std::vector<uint64_t> keys(s);
     std::vector<uint8_t> flags(s);
+    std::vector<uint32_t> uoff(s);
     PinnedBuf buf;
     HIP_TRY(hipHostMalloc((void**)&buf.p, kIoChunk, hipHostMallocDefault));
     Fnv hash;
@@ -1501,9 +1571,14 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
             if (si == 2) std::memcpy(reinterpret_cast<uint8_t*>(keys.data()) + off, buf.p, c);
             if (si == 3) std::memcpy(flags.data() + off, buf.p, c);
             if (si == 4) std::memcpy(reinterpret_cast<uint8_t*>(h->h_levels.data()) + off, buf.p, c);
+            if (si == 6) std::memcpy(reinterpret_cast<uint8_t*>(uoff.data()) + off, buf.p, c);
+            if ((si == 5 || si == 7) && !adj_ids_ok(reinterpret_cast<const uint32_t*>(buf.p), c / 4, s))
+                return fail(VSG_EINVAL, "vsg index file: adjacency id out of range");
         }
     }
     if (hash.h != fh.payload_hash) return fail(VSG_EINVAL, "vsg index file payload checksum mismatch");
+    if ((rc = validate_graph(s, h->h_levels.data(), uoff.data(), fh.upper_rows, fh.entry, fh.max_level,
+                                 (h->opt.flags & VSG_FLAG_EXACT_ONLY) != 0))) return rc;
     h->slots = s;
     h->upper_used = fh.upper_rows;
     h->entry = fh.entry;
@@ -1512,7 +1587,8 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
     h->keys.reserve(fh.live);
     for (size_t i = 0; i < s; ++i)
         if (!(flags[i] & 1)) {
-            if (!h->keys.insert(keys[i], (uint32_t)i)) return fail(VSG_EINVAL, "vsg index file has duplicate live keys");
+            if (!h->keys.insert(keys[i], (uint32_t)i))
+                return fail(VSG_EINVAL, "vsg index file has a reserved or duplicate live key");
             h->live++;
         }
     if (h->live != fh.live) return fail(VSG_EINVAL, "vsg index file live count mismatch");

@@ -377,7 +377,7 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
     std::vector<uint32_t> order(n);
     std::vector<int8_t> blev(n);
     for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
-    {
+    if (env_double("VSG_BUILD_PERMUTE", 1) != 0) {  // 0: slot order (tests: sequential-build identity)
         const uint64_t base = host_splitmix64(h->opt.seed ^ 0x5045524D55544Eull ^ (uint64_t)s0);
         for (size_t i = n; i > 1; --i) {
             const size_t j = (size_t)(host_splitmix64(base + i) % i);
@@ -392,6 +392,9 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
     HIP_TRY(hipMemcpyAsync(h->d_blevels, blev.data(), n, hipMemcpyHostToDevice, st));
 
     const double frac = env_double("VSG_BUILD_BATCH_FRAC", 1.0 / 16.0);
+    // probe knobs: a second batch fraction once the graph holds `switch_at` nodes
+    const double frac2 = env_double("VSG_BUILD_BATCH_FRAC2", frac);
+    const double switch_at = env_double("VSG_BUILD_BATCH_SWITCH", 0);
     const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 32768);
     // at least 8 batches per call, so the call's own nodes find each other
     const size_t bcall = std::max<size_t>(1, n / 8);
@@ -405,7 +408,7 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
     }
     while (i < n) {
         const size_t graph_nodes = (size_t)h->slots - n + i;
-        size_t b = (size_t)std::floor((double)graph_nodes * frac);
+        size_t b = (size_t)std::floor((double)graph_nodes * (switch_at > 0 && graph_nodes >= switch_at ? frac2 : frac));
         b = std::max<size_t>(1, std::min(std::min(b, bmax), bcall));
         b = std::min(b, n - i);
         int new_top = -1;

@@ -51,9 +51,9 @@ def test_invalid_options_rejected_without_device():
     rc = vsg.lib().vsg_index_new(C.byref(opt), C.byref(h))
     assert rc == _lib.VSG_EINVAL and not h.value
     assert b"dimensions" in vsg.lib().vsg_last_error()
-    opt = _lib.Options(8, 0, 0, 64, 0, 0, 0, 0, 0)
+    opt = _lib.Options(8, 0, 0, 65, 0, 0, 0, 0, 0)  # connectivity: [2, 64]
     rc = vsg.lib().vsg_index_new(C.byref(opt), C.byref(h))
-    assert rc == _lib.VSG_EUNSUPPORTED
+    assert rc == _lib.VSG_EUNSUPPORTED and b"connectivity" in vsg.lib().vsg_last_error()
 
 
 def test_no_silent_fallback_when_library_missing(monkeypatch, tmp_path):

@@ -272,6 +272,29 @@ def test_hnsw_forgetful_visited_table_is_exact(monkeypatch):
     np.testing.assert_array_equal(graphs[0]["upper"], graphs[1]["upper"])
 
 
+@pytest.mark.parametrize("metric,dim,M,efc", [("l2sq", 32, 8, 64), ("ip", 48, 16, 128), ("l2sq", 128, 16, 300)])
+def test_hnsw_gpu_build_one_node_batches_equals_oracle_graph(metric, dim, M, efc, monkeypatch):
+    """With one node per batch and insertion in slot order (debug knobs), the GPU build
+    kernels (insert: descent, efC beam, refine_ heuristic; sort; reverse links with
+    heuristic re-selection) must reproduce the oracle's sequential usearch build
+    (oracle/vsg_oracle.c insert_slot) graph bit for bit on integer data -- every
+    level-0 and upper row, levels and entry point.  The production build differs only
+    in batching (nodes of one batch do not see each other), bounded by recall tests."""
+    n = 1500
+    div = 16.0 if metric == "ip" else 1.0
+    x = np.floor(G.uint8_valued(n, dim, 33) / div).astype(np.float32)
+    monkeypatch.setenv("VSG_BUILD_PERMUTE", "0")
+    monkeypatch.setenv("VSG_BUILD_BATCH_MAX", "1")
+    gpu = vsg.Index(dim, metric, "f32", M, efc, 64, seed=21)
+    gpu.add(np.arange(n), x)
+    h = O.HnswOracle(dim, metric, M, efc, 64, seed=21)
+    h.add(np.arange(n), x, threads=1)
+    a, b = gpu.export(), h.export()
+    assert (a["entry"], a["max_level"]) == (b["entry"], b["max_level"])
+    for key in ("levels", "upper_off", "adj0", "upper"):
+        np.testing.assert_array_equal(a[key], b[key], err_msg=key)
+
+
 @pytest.mark.parametrize("metric,dim,quant", [("l2sq", 64, "f32"), ("cos", 128, "f32"),
                                               ("ip", 96, "f32"), ("l2sq", 64, "f16"),
                                               ("cos", 384, "f32"), ("cos", 768, "f16")])

@@ -111,6 +111,7 @@ hipError_t launch_exact(Storage st, MetricKind mk, const ExactParams& p, hipStre
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, p.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(exact_kernel, sh, tt, mt);
+        if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3(p.nq, p.nblocks), dim3(64), lds, s, p);
         err = hipGetLastError();
     });
@@ -119,7 +120,10 @@ hipError_t launch_exact(Storage st, MetricKind mk, const ExactParams& p, hipStre
 
 hipError_t launch_merge_parts(const MergeParams& p, hipStream_t s) {
     if (p.nq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(merge_parts_kernel, dim3(p.nq), dim3(64), exact_lds_bytes(p.k), s, p);
+    const size_t lds = exact_lds_bytes(p.k);
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)merge_parts_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(merge_parts_kernel, dim3(p.nq), dim3(64), lds, s, p);
     return hipGetLastError();
 }
 

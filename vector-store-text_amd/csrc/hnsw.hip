@@ -36,9 +36,9 @@ __host__ __device__ int hash_size_for(int ef, int factor) {
 
 // cooperative search: + 8 control words (WgCtl) after the shared wave state
 size_t search_lds_bytes(int ef, int hash, int waves) {
-    return wave_lds_bytes(hash, ef, false) + (waves > 1 ? 32 : 0);
+    return wave_lds_bytes(hash, ef, 0) + (waves > 1 ? 32 : 0);
 }
-size_t insert_lds_bytes(int efc, int hash) { return wave_lds_bytes(hash, efc, true); }
+size_t insert_lds_bytes(int efc, int hash, int m0) { return wave_lds_bytes(hash, efc, sel_entries(m0)); }
 
 
 // usearch search_to_find_in_base_ restated (oracle beam()).
@@ -73,29 +73,34 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
         if (lane == 0) L.I()[p] = node | VSG_EXP_BIT;
         hint = p + 1;
         const uint32_t* row = g.row(node, l);
-        const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
         ++nadj;
-        bool fresh = false, evicted = false;
-        if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
-        const uint64_t mask = __ballot(fresh);
-        lossy = lossy || __ballot(evicted) != 0;
-        const int cnt = popc64(mask);
-        if (fresh) w.todo[lanes_below(mask)] = nb;
-        wave_sync();
-        const uint64_t t1 = VSG_CLK();
-        pf.adj += t1 - t0;
-        if (cnt == 0) continue;
-        rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
-        wave_sync();
-        ndist += (uint64_t)cnt;
-        const bool valid = lane < cnt;
-        const float cd = valid ? w.tdist[lane] : 0.f;
-        const uint32_t ci = valid ? w.todo[lane] : 0u;
-        wave_sync();
-        const uint64_t t2 = VSG_CLK();
-        pf.dist += t2 - t1;
-        hint = min(hint, L.merge(valid, cd, ci, lossy, w.sd, w.si));
-        pf.merge += VSG_CLK() - t2;
+        for (int c0 = 0; c0 < m; c0 += 64) {  // 64-entry pieces of the row (M0 <= 128)
+            const uint32_t nb = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
+            const bool full = __ballot(nb != VSG_EMPTY) == ~0ull;
+            bool fresh = false, evicted = false;
+            if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
+            const uint64_t mask = __ballot(fresh);
+            lossy = lossy || __ballot(evicted) != 0;
+            const int cnt = popc64(mask);
+            if (fresh) w.todo[lanes_below(mask)] = nb;
+            wave_sync();
+            const uint64_t t1 = VSG_CLK();
+            pf.adj += t1 - t0;
+            if (cnt) {
+                rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
+                wave_sync();
+                ndist += (uint64_t)cnt;
+                const bool valid = lane < cnt;
+                const float cd = valid ? w.tdist[lane] : 0.f;
+                const uint32_t ci = valid ? w.todo[lane] : 0u;
+                wave_sync();
+                const uint64_t t2 = VSG_CLK();
+                pf.dist += t2 - t1;
+                hint = min(hint, L.merge(valid, cd, ci, lossy, w.sd, w.si));
+                pf.merge += VSG_CLK() - t2;
+            }
+            if (!full) break;
+        }
     }
 }
 
@@ -187,7 +192,7 @@ __global__ __launch_bounds__(64) void hnsw_search_kernel(SearchParams p) {
     }
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
-    WaveLds w = carve(smem, p.ef, p.hash_size, false);
+    WaveLds w = carve(smem, p.ef, p.hash_size, 0);
     uint64_t ndist = 0, nadj = 0;
     BeamProf pf;
     int count = 0;
@@ -339,8 +344,8 @@ __global__ __launch_bounds__(64 * NW) void hnsw_search_wg_kernel(SearchParams p)
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
-    WaveLds w = carve(smem, p.ef, p.hash_size, false);
-    int* ctl = reinterpret_cast<int*>(smem + wave_lds_bytes(p.hash_size, p.ef, false));
+    WaveLds w = carve(smem, p.ef, p.hash_size, 0);
+    int* ctl = reinterpret_cast<int*>(smem + wave_lds_bytes(p.hash_size, p.ef, 0));
     uint64_t ndist = 0, nadj = 0;
     [[maybe_unused]] BeamProf pf;
     int count = 0;
@@ -410,7 +415,7 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     const int bi = blockIdx.x;
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
-    WaveLds w = carve(smem, p.efc, p.hash_size, true);
+    WaveLds w = carve(smem, p.efc, p.hash_size, sel_entries(g.M0));
     const uint64_t t_start = wall_clock64();
     const uint32_t node = p.nodes[bi];
     const int L = p.levels[bi];
@@ -436,12 +441,12 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
         const int m = l == 0 ? g.M0 : g.M;
         const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, m, nsel_d);
         uint32_t* row = g.row(node, l);
-        if (lane < m) row[lane] = lane < nsel ? w.sel[lane] : VSG_EMPTY;
-        if (lane < nsel) {
-            const uint64_t key = ((uint64_t)l << PAIR_L_SHIFT) | ((uint64_t)w.sel[lane] << PAIR_V_SHIFT) |
+        for (int j = lane; j < m; j += 64) row[j] = j < nsel ? w.sel[j] : VSG_EMPTY;
+        for (int j = lane; j < nsel; j += 64) {
+            const uint64_t key = ((uint64_t)l << PAIR_L_SHIFT) | ((uint64_t)w.sel[j] << PAIR_V_SHIFT) |
                                  (uint64_t)node;
-            p.pair_keys[pos + lane] = key;
-            p.pair_vals[pos + lane] = __float_as_uint(w.seld[lane]);
+            p.pair_keys[pos + j] = key;
+            p.pair_vals[pos + j] = __float_as_uint(w.seld[j]);
         }
         pos += (uint32_t)nsel;
         cur = w.list.I()[0] & VSG_ID_MASK;
@@ -473,7 +478,7 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
     const int cap = 2 * g.M0 > 64 ? 2 * g.M0 : 64;
-    WaveLds w = carve(smem, cap, hash_size_for(cap, 32), true);
+    WaveLds w = carve(smem, cap, hash_size_for(cap, 32), sel_entries(g.M0));
     const uint64_t t_start = wall_clock64();
     uint64_t ndist = 0, nadj = 0, nsel_d = 0, nprune = 0, nappend = 0;
     const size_t nw = gridDim.x;
@@ -509,10 +514,14 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
             const int nin = (int)(e - h);
             const int m = l == 0 ? g.M0 : g.M;
             uint32_t* row = g.row(v, l);
-            const uint32_t x = lane < m ? row[lane] : VSG_EMPTY;
             ++nadj;
-            const uint64_t xm = __ballot(x != VSG_EMPTY);
-            const int ne = popc64(xm);
+            int ne = 0;  // rows are a compact prefix (M0 <= 128: up to two pieces)
+            for (int c0 = 0; c0 < m; c0 += 64) {
+                const uint32_t x = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
+                const uint64_t xm = __ballot(x != VSG_EMPTY);
+                ne += popc64(xm);
+                if (xm != ~0ull) break;
+            }
             if (ne + nin <= m) {
                 for (int t = lane; t < nin; t += 64) row[ne + t] = (uint32_t)(p.keys[h + t] & PAIR_ID_MASK);
                 ++nappend;
@@ -524,13 +533,16 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
             List& L = w.list;
             L.cur = 0;
             L.size = 0;
-            if (x != VSG_EMPTY) w.todo[lanes_below(xm)] = x;
-            wave_sync();
-            rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, ne, q, w.tdist);
-            wave_sync();
-            ndist += (uint64_t)ne;
-            {
-                const bool valid = lane < ne;
+            for (int c0 = 0; c0 < ne; c0 += 64) {  // existing neighbours, distances recomputed
+                const uint32_t x = c0 + lane < ne ? row[c0 + lane] : VSG_EMPTY;
+                const uint64_t xm = __ballot(x != VSG_EMPTY);
+                const int c = popc64(xm);
+                if (x != VSG_EMPTY) w.todo[lanes_below(xm)] = x;
+                wave_sync();
+                rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, c, q, w.tdist);
+                wave_sync();
+                ndist += (uint64_t)c;
+                const bool valid = lane < c;
                 const float cd = valid ? w.tdist[lane] : 0.f;
                 const uint32_t ci = valid ? w.todo[lane] : 0u;
                 wave_sync();
@@ -544,7 +556,7 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
                 L.merge(valid, cd, ci, false, w.sd, w.si);
             }
             const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, L.size, m, nsel_d);
-            if (lane < m) row[lane] = lane < nsel ? w.sel[lane] : VSG_EMPTY;
+            for (int j = lane; j < m; j += 64) row[j] = j < nsel ? w.sel[j] : VSG_EMPTY;
             wave_sync();
         }
     }
@@ -567,8 +579,12 @@ bool shape_supported(int nchunks) { return nchunks >= 1 && nchunks <= 1024; }
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s) {
     if (p.nq <= 0) return hipSuccess;
-    if (p.reg || p.upper_ef > 1) return launch_search_reg(st, mk, p, s);  // multi-entry: reg kernel only
-    const int nw = p.waves == 2 || p.waves == 4 ? p.waves : 1;
+    // register kernel up to ef 1024 (multi-entry descent: register kernel only);
+    // above it the sorted LDS list (ef <= MAX_EF)
+    if ((p.reg && p.ef <= (int)MAX_REG_EF) || p.upper_ef > 1) return launch_search_reg(st, mk, p, s);
+    if (p.ef < 1 || p.ef > (int)MAX_EF || p.k > p.ef) return hipErrorInvalidValue;
+    // the cooperative kernel stages one 64-entry row piece per expansion: M0 <= 64 only
+    const int nw = (p.waves == 2 || p.waves == 4) && p.g.M0 <= 64 ? p.waves : 1;
     const size_t lds = search_lds_bytes(p.ef, p.hash_size, nw);
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
@@ -600,7 +616,7 @@ hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipSt
 
 hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s) {
     if (p.nnodes <= 0) return hipSuccess;
-    const size_t lds = insert_lds_bytes(p.efc, p.hash_size);
+    const size_t lds = insert_lds_bytes(p.efc, p.hash_size, p.g.M0);
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(hnsw_insert_kernel, sh, tt, mt);
@@ -614,7 +630,7 @@ hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipSt
 hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s) {
     if (p.npairs == 0) return hipSuccess;
     const int cap = 2 * p.g.M0 > 64 ? 2 * p.g.M0 : 64;
-    const size_t lds = insert_lds_bytes(cap, hash_size_for(cap, 32));
+    const size_t lds = insert_lds_bytes(cap, hash_size_for(cap, 32), p.g.M0);
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(hnsw_reverse_kernel, sh, tt, mt);

@@ -8,8 +8,10 @@
 
 namespace vsg {
 
-static inline __host__ __device__ size_t wave_lds_bytes(int hash, int cap, bool with_sel) {
-    return (size_t)hash * 4 + (size_t)cap * 16 + 64 * 4 * 4 + (with_sel ? 64 * 4 * 2 : 0);
+// sel: entries of the heuristic-selection output (0 = none; >= M0 for the build)
+static inline __host__ __device__ int sel_entries(int m0) { return m0 > 64 ? m0 : 64; }
+static inline __host__ __device__ size_t wave_lds_bytes(int hash, int cap, int sel) {
+    return (size_t)hash * 4 + (size_t)cap * 16 + 64 * 4 * 4 + (size_t)sel * 4 * 2;
 }
 
 static __device__ inline GraphDev to_dev(const DevGraph& g) {
@@ -36,7 +38,7 @@ struct WaveLds {
     float* seld;
 };
 
-static __device__ inline WaveLds carve(uint8_t* smem, int cap, int hs, bool with_sel) {
+static __device__ inline WaveLds carve(uint8_t* smem, int cap, int hs, int sel) {
     WaveLds w;
     uint8_t* p = smem;
     w.vis.tab = reinterpret_cast<uint32_t*>(p);
@@ -61,11 +63,11 @@ static __device__ inline WaveLds carve(uint8_t* smem, int cap, int hs, bool with
     p += 256;
     w.tdist = reinterpret_cast<float*>(p);
     p += 256;
-    if (with_sel) {
+    if (sel) {
         w.sel = reinterpret_cast<uint32_t*>(p);
-        p += 256;
+        p += (size_t)sel * 4;
         w.seld = reinterpret_cast<float*>(p);
-        p += 256;
+        p += (size_t)sel * 4;
     } else {
         w.sel = nullptr;
         w.seld = nullptr;
@@ -86,7 +88,9 @@ __device__ inline float dist_one(const GraphDev& g, const QReg<G, VM, T>& q, uin
 }
 
 // usearch search_for_one_ restated (oracle greedy()): move to the best
-// neighbour (lexicographic (distance, slot)) until none improves.
+// neighbour (lexicographic (distance, slot)) until none improves.  Rows longer
+// than a wave (M0 = 2M > 64, M <= 64) are read in 64-entry pieces; rows are a
+// compact prefix, so a piece that ends in EMPTY ends the row (oracle read_row).
 template <int G, int VM, int U, typename T, int MET>
 __device__ void greedy_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t& cur,
                              float& dcur, WaveLds& w, uint64_t& ndist, uint64_t& nadj) {
@@ -94,22 +98,31 @@ __device__ void greedy_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, 
     const int m = l == 0 ? g.M0 : g.M;
     for (;;) {
         const uint32_t* row = g.row(cur, l);
-        const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
-        const bool ok = nb != VSG_EMPTY;
-        const uint64_t mask = __ballot(ok);
-        const int cnt = popc64(mask);
+        float d = __builtin_inff();
+        uint32_t id = VSG_EMPTY;
         ++nadj;
-        if (ok) w.todo[lanes_below(mask)] = nb;
-        wave_sync();
-        if (cnt == 0) break;
-        rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
-        wave_sync();
-        ndist += (uint64_t)cnt;
-        float d = lane < cnt ? w.tdist[lane] : __builtin_inff();
-        uint32_t id = lane < cnt ? w.todo[lane] : VSG_EMPTY;
-        wave_sync();
+        for (int c0 = 0; c0 < m; c0 += 64) {
+            const uint32_t nb = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
+            const bool ok = nb != VSG_EMPTY;
+            const uint64_t mask = __ballot(ok);
+            const int cnt = popc64(mask);
+            if (ok) w.todo[lanes_below(mask)] = nb;
+            wave_sync();
+            if (cnt == 0) break;
+            rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
+            wave_sync();
+            ndist += (uint64_t)cnt;
+            const float cd = lane < cnt ? w.tdist[lane] : __builtin_inff();
+            const uint32_t ci = lane < cnt ? w.todo[lane] : VSG_EMPTY;
+            if (cand_less(cd, ci, d, id)) {
+                d = cd;
+                id = ci;
+            }
+            wave_sync();
+            if (cnt < 64) break;
+        }
         wave_argmin(d, id);
-        if (cand_less(d, id, dcur, cur)) {
+        if (id != VSG_EMPTY && cand_less(d, id, dcur, cur)) {
             cur = id;
             dcur = d;
         } else {

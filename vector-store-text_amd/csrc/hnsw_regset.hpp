@@ -253,26 +253,34 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
         B.mark_expanded(a);
         const uint32_t na = (uint32_t)a & VSG_ID_MASK;
         const uint32_t* row = l == 0 ? adj0 + (size_t)na * m0r : upper + ((size_t)upper_off[na] + (size_t)(l - 1)) * mr;
-        const uint32_t nb = lane < m ? row[lane] : VSG_EMPTY;
         ++nadj;
-        bool fresh = false, evicted = false;
-        if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
-        const uint64_t mask = __ballot(fresh);
-        lossy = lossy || __ballot(evicted) != 0;
-        const int cnt = popc64(mask);
-        if (fresh) w.todo[lanes_below(mask)] = nb;
-        wave_sync();
-        const uint64_t t1 = VSG_CLK();
-        pf.adj += t1 - t0;
-        if (cnt == 0) continue;
-        rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
-        wave_sync();
-        ndist += (uint64_t)cnt;
-        const uint64_t ck = lane < cnt ? cand_key(w.tdist[lane], w.todo[lane]) : VSG_KEY_EMPTY;
-        const uint64_t t2 = VSG_CLK();
-        pf.dist += t2 - t1;
-        admit<R>(B, lane < cnt, ck, lossy, ef, sk);
-        pf.merge += VSG_CLK() - t2;
+        // one 64-entry piece of the row per pass (M0 = 2M <= 128); the expansion's
+        // pieces are admitted one after another, which leaves the same set as one
+        // batch (B only ever keeps the best ef of everything evaluated)
+        for (int c0 = 0; c0 < m; c0 += 64) {
+            const uint32_t nb = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
+            const bool full = __ballot(nb != VSG_EMPTY) == ~0ull;
+            bool fresh = false, evicted = false;
+            if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
+            const uint64_t mask = __ballot(fresh);
+            lossy = lossy || __ballot(evicted) != 0;
+            const int cnt = popc64(mask);
+            if (fresh) w.todo[lanes_below(mask)] = nb;
+            wave_sync();
+            const uint64_t t1 = VSG_CLK();
+            pf.adj += t1 - t0;
+            if (cnt) {
+                rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
+                wave_sync();
+                ndist += (uint64_t)cnt;
+                const uint64_t ck = lane < cnt ? cand_key(w.tdist[lane], w.todo[lane]) : VSG_KEY_EMPTY;
+                const uint64_t t2 = VSG_CLK();
+                pf.dist += t2 - t1;
+                admit<R>(B, lane < cnt, ck, lossy, ef, sk);
+                pf.merge += VSG_CLK() - t2;
+            }
+            if (!full) break;  // compact prefix: the row ended inside this piece
+        }
     }
 }
 

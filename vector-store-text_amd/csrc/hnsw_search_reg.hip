@@ -45,7 +45,7 @@ __global__ __launch_bounds__(64) void hnsw_search_reg_kernel(SearchParams p) {
     }
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
-    WaveLds w = carve(smem, 0, p.hash_size, false);
+    WaveLds w = carve(smem, 0, p.hash_size, 0);
     uint64_t ndist = 0, nadj = 0;
     BeamProf pf;
     int count = 0;
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(64) void hnsw_search_reg_kernel(SearchParams p) {
 // slots per lane: 64 R >= ef + 64 (a compaction leaves room for a full batch)
 static inline int reg_rows(int ef) { return ef <= 64 ? 2 : ef <= 192 ? 4 : ef <= 448 ? 8 : 17; }
 
-size_t search_reg_lds_bytes(int hash) { return wave_lds_bytes(hash, 0, false); }
+size_t search_reg_lds_bytes(int hash) { return wave_lds_bytes(hash, 0, 0); }
 
 hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s) {
     if (p.nq <= 0) return hipSuccess;

@@ -309,7 +309,7 @@ struct Visited {
 };
 
 // ------------------------------------------------------------- sorted list --
-// (distance, slot) ascending; slot high bit = "expanded".  cap <= 1024.
+// (distance, slot) ascending; slot high bit = "expanded".  cap <= MAX_EF (4096).
 
 struct List {
     float* d0;

@@ -486,9 +486,19 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
 // EMPTY, levels are in [0, 30], upper rows of each slot lie inside the upper
 // table, the entry point is a slot on the top level.  The search kernels index
 // HBM with these values, so nothing else guards them.
-static bool adj_ids_ok(const uint32_t* ids, size_t n, size_t slots) {
-    for (size_t i = 0; i < n; ++i)
-        if (ids[i] != 0xFFFFFFFFu && ids[i] >= slots) return false;
+// ids: rows of `width` entries, each a compact prefix of slot ids with EMPTY
+// after it.  `first` = index of ids[0] in the whole table; `prev_empty` carries
+// the previous element's state across calls (streamed load).
+static bool adj_ids_ok(const uint32_t* ids, size_t n, size_t slots, size_t width, size_t first = 0,
+                       bool* prev_empty = nullptr) {
+    bool pe = prev_empty ? *prev_empty : false;
+    for (size_t i = 0; i < n; ++i) {
+        const bool row_start = (first + i) % width == 0;
+        const bool e = ids[i] == 0xFFFFFFFFu;
+        if (!e && (ids[i] >= slots || (!row_start && pe))) return false;  // out of range, or a hole
+        pe = e;
+    }
+    if (prev_empty) *prev_empty = pe;
     return true;
 }
 
@@ -532,7 +542,8 @@ int vsg_index_new(const vsg_index_options_t* o, vsg_index_t** out) {
     if (o->metric > VSG_METRIC_COS) return fail(VSG_EINVAL, "unknown metric");
     if (o->quantization > VSG_SCALAR_F16) return fail(VSG_EINVAL, "unknown quantization");
     const uint32_t M = o->connectivity ? o->connectivity : 16;
-    if (M < 2 || M > 32) return fail(VSG_EUNSUPPORTED, "connectivity must be in [2, 32]");
+    if (M < 2 || M > (uint32_t)MAX_CONNECTIVITY)
+        return fail(VSG_EUNSUPPORTED, "connectivity must be in [2, " + std::to_string(MAX_CONNECTIVITY) + "]");
     auto* h = new vsg_index();
     h->opt = *o;
     h->dim = (int)o->dimensions;
@@ -543,7 +554,11 @@ int vsg_index_new(const vsg_index_options_t* o, vsg_index_t** out) {
     h->M0 = 2 * (int)M;
     h->efc = o->expansion_add ? (int)o->expansion_add : 128;
     h->ef = o->expansion_search ? (int)o->expansion_search : 64;
-    if (h->efc > 1024) h->efc = 1024;
+    if (h->efc > (int)MAX_EF) {
+        delete h;
+        return fail(VSG_EUNSUPPORTED, "expansion_add > " + std::to_string(MAX_EF) +
+                                          " is not supported (the build beam keeps its efC list in LDS)");
+    }
     h->elem = h->st == ST_F16 ? 2 : 4;
     h->f16_trav = (o->flags & VSG_FLAG_F16_TRAVERSAL) != 0;
     if (h->f16_trav && h->st != ST_F32) {
@@ -805,9 +820,20 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
                                 uint64_t* ok, float* od, uint32_t* oc, hipStream_t s, bool exact) {
     if (k == 0) return fail(VSG_EINVAL, "k must be >= 1 (Limit is NonZeroUsize)");
     if (nq == 0) return VSG_OK;
-    if (k > 1024) return fail(VSG_EUNSUPPORTED, "k > 1024");
     if (!exact && (h->opt.flags & VSG_FLAG_EXACT_ONLY))
         return fail(VSG_EUNSUPPORTED, "index was created with VSG_FLAG_EXACT_ONLY (no graph)");
+    // no silent clamps: every limit of the kernels is an explicit error
+    const size_t ef_eff = std::max(ef ? ef : (size_t)h->ef, k);  // usearch: max(expansion, wanted)
+    if (exact && k > MAX_EXACT_K)
+        return fail(VSG_EUNSUPPORTED, "k > " + std::to_string(MAX_EXACT_K) + " is not supported by exact search");
+    if (!exact && ef_eff > MAX_EF)
+        return fail(VSG_EUNSUPPORTED, "HNSW search with max(ef, k) = " + std::to_string(ef_eff) + " > " +
+                                          std::to_string(MAX_EF) + " is not supported (the beam lives in LDS)");
+    if (!exact && h->f16_trav && ef_eff > MAX_REG_EF)
+        return fail(VSG_EUNSUPPORTED, "f16 traversal + re-rank supports max(ef, k) <= " + std::to_string(MAX_REG_EF));
+    const int upper_ef = (int)env_double("VSG_SEARCH_UPPER_EF", h->upper_ef);
+    if (!exact && upper_ef > 1 && ef_eff > MAX_REG_EF)
+        return fail(VSG_EUNSUPPORTED, "multi-entry descent (upper_ef) supports max(ef, k) <= " + std::to_string(MAX_REG_EF));
     // exact search on the f32 matrix cores when the batch amortises a 128-query tile
     const size_t mfma_min = (size_t)env_double("VSG_EXACT_MFMA_MIN", 32);
     const bool use_mfma = exact && h->st == ST_F32 && k <= 16 && (h->row_bytes / 4) % 32 == 0 &&
@@ -828,14 +854,16 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
     } else if (exact) {
         // grid.y = row blocks (<= 65535 per dimension)
         nblocks = (int)std::min<size_t>(32768, std::max<size_t>(1, (slots + 4095) / 4096));
+        // large k: bound the partial lists (nq x nblocks x k x 8 B) to ~1 GiB
+        const size_t cap_blocks = std::max<size_t>(1, ((size_t)1 << 30) / (8 * nq * k));
+        nblocks = (int)std::min<size_t>((size_t)nblocks, cap_blocks);
         rpb = (int)((slots + nblocks - 1) / nblocks);
         if (slots == 0) nblocks = 1;
         np = nq * (size_t)nblocks * k;
     }
     // f16 traversal: the beam (ef slots) of the f16 search is re-ranked in f32
     const bool rerank = !exact && h->f16_trav && h->slots > 0;
-    size_t efr = ef ? ef : (size_t)h->ef;
-    efr = std::min<size_t>(std::max(efr, k), 1024);
+    const size_t efr = ef_eff;
     size_t rr_b = 0;
     if (rerank) {
         int rc0 = ensure_shadow(h, s);
@@ -890,9 +918,7 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
             err = launch_merge_parts(gp, s);
         }
     } else if (err == hipSuccess && !exact) {
-        size_t e = ef ? ef : (size_t)h->ef;
-        e = std::max(e, k);
-        if (e > 1024) e = 1024;
+        const size_t e = ef_eff;
         SearchParams p{};
         p.g = h->graph();
         p.queries = qp;
@@ -925,7 +951,7 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         // +12-46% at ef >= 192, profiles/r01_search_phases.jsonl);
         // VSG_SEARCH_REG=0 selects the LDS-list kernels
         p.reg = env_double("VSG_SEARCH_REG", 1) != 0 ? 1 : 0;
-        p.upper_ef = (int)env_double("VSG_SEARCH_UPPER_EF", h->upper_ef);
+        p.upper_ef = upper_ef;
         if (!rerank) {
             err = launch_search(h->st, h->mk, p, s);
         } else {
@@ -1246,7 +1272,7 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
     int rc = validate_graph(slots, levels, upper_off, upper_rows, entry, max_level,
                             (h->opt.flags & VSG_FLAG_EXACT_ONLY) != 0);
     if (rc) return rc;
-    if (!adj_ids_ok(adj0, slots * h->M0, slots) || !adj_ids_ok(upper, upper_rows * h->M, slots))
+    if (!adj_ids_ok(adj0, slots * h->M0, slots, h->M0) || !adj_ids_ok(upper, upper_rows * h->M, slots, h->M))
         return fail(VSG_EINVAL, "import: adjacency id out of range");
     {
         KeyMap probe;
@@ -1428,7 +1454,7 @@ int read_header(FILE* f, FileHeader& fh, size_t* file_bytes) {
     if (fh.version != kFileVersion || fh.header_bytes != sizeof(FileHeader))
         return fail(VSG_EUNSUPPORTED, "unsupported vsg index file version " + std::to_string(fh.version));
     if (header_hash(fh) != fh.header_hash) return fail(VSG_EINVAL, "vsg index file header checksum mismatch");
-    if (fh.M0 != 2 * fh.M || fh.M < 2 || fh.M > 32 || fh.live > fh.slots || fh.slots > MAX_SLOTS)
+    if (fh.M0 != 2 * fh.M || fh.M < 2 || fh.M > (uint32_t)MAX_CONNECTIVITY || fh.live > fh.slots || fh.slots > MAX_SLOTS)
         return fail(VSG_EINVAL, "vsg index file header is inconsistent");
     if ((size_t)sz != sizeof(FileHeader) + payload_bytes(fh))
         return fail(VSG_EINVAL, "vsg index file size does not match its header (truncated?)");
@@ -1563,6 +1589,7 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
     const std::vector<Section> secs = sections(h, s, fh.upper_rows);
     for (size_t si = 0; si < secs.size(); ++si) {
         const Section& sec = secs[si];
+        bool prev_empty = false;
         for (size_t off = 0; off < sec.bytes; off += kIoChunk) {
             const size_t c = std::min(kIoChunk, sec.bytes - off);
             if (std::fread(buf.p, 1, c, fc.f) != c) return fail(VSG_EINVAL, "read failed (truncated payload)");
@@ -1575,7 +1602,8 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
             if (si == 3) std::memcpy(flags.data() + off, buf.p, c);
             if (si == 4) std::memcpy(reinterpret_cast<uint8_t*>(h->h_levels.data()) + off, buf.p, c);
             if (si == 6) std::memcpy(reinterpret_cast<uint8_t*>(uoff.data()) + off, buf.p, c);
-            if ((si == 5 || si == 7) && !adj_ids_ok(reinterpret_cast<const uint32_t*>(buf.p), c / 4, s))
+            if ((si == 5 || si == 7) && !adj_ids_ok(reinterpret_cast<const uint32_t*>(buf.p), c / 4, s,
+                                                     si == 5 ? fh.M0 : fh.M, off / 4, &prev_empty))
                 return fail(VSG_EINVAL, "vsg index file: adjacency id out of range");
         }
     }

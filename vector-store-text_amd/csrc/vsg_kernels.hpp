@@ -126,11 +126,16 @@ constexpr int PAIR_V_SHIFT = 29;
 constexpr int PAIR_L_SHIFT = 58;
 constexpr uint64_t PAIR_ID_MASK = (1ull << 29) - 1;
 constexpr uint32_t MAX_SLOTS = 1u << 29;
+// Limits of the kernels (explicit VSG_EUNSUPPORTED above them, never a clamp):
+constexpr size_t MAX_EF = 4096;       // search ef / build efC: sorted list in LDS (16 B per entry)
+constexpr size_t MAX_REG_EF = 1024;   // register candidate set (hnsw_search_reg.hip), re-rank beam
+constexpr size_t MAX_EXACT_K = 8192;  // exact search: per-block top-k list in LDS
+constexpr int MAX_CONNECTIVITY = 64;  // M; level-0 rows of M0 = 2M <= 128 entries
 
 bool shape_supported(int nchunks);
 __host__ __device__ int hash_size_for(int ef, int factor);
 size_t search_lds_bytes(int ef, int hash, int waves = 1);
-size_t insert_lds_bytes(int efc, int hash);
+size_t insert_lds_bytes(int efc, int hash, int m0);
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
 hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);

@@ -8,15 +8,16 @@ resident in HBM) at the smallest ef whose recall@10 against exact ground truth i
 >= 0.95 (ef swept on a 1,000-query subset).
 
 N > 1 (--multi both, default) measures two legs in one run:
-  * replica (`value`): every rank holds the whole 1M index (3 GB of 288 GB HBM)
-    and serves its own 10,000-query batch per step; per-GPU work fixed =>
-    "scaling": "weak", value = all ranks' queries / max-over-ranks time.
-  * shard (`shard_mode`, the north-star layout): rank r owns rows
-    [r N/G, (r+1) N/G), every query is searched on every shard, per-shard top-k'
+  * shard (`value`, the north-star layout): rank r owns rows [r N/G, (r+1) N/G)
+    of the 1M index, every query is searched on every shard, the per-shard top-k'
     is all-gathered over RCCL (xGMI) and k-way merged by the HIP merge kernel;
-    (ef, k') re-tuned for merged recall; total work fixed => strong scaling.
-DESIGN.md §6 explains why replicas, not shards, maximise QPS when the index fits
-one GPU, and why shards still win the build.
+    (ef, k') re-tuned for merged recall >= 0.95; total work fixed => "scaling":
+    "strong", value = queries / max-over-ranks time.  The build is sharded too
+    (every rank builds N/G rows, no communication).
+  * replica (`replica_mode`, beside it): every rank holds the whole 1M index
+    (3 GB of 288 GB HBM) and serves its own 10,000-query batch per step (weak).
+DESIGN.md §6 explains why replicas maximise QPS when the index fits one GPU and
+shards win the build; the headline follows the north star's layout.
 
 Also reported: build vectors/s (GPU batched HNSW build of the whole index, max over
 ranks), the HBM roofline of the search kernel (algorithmic bytes counted by the
@@ -338,7 +339,7 @@ def hnsw_leg(c, mode):
         "build_dist_per_vector": bstats["build_distances"] / max(1, nloc),
         # algorithmic bytes of the whole build: every distance evaluation reads one
         # row, every adjacency visit one 2M-entry level-0 row (upper rows are shorter)
-        "build_alg_bytes": bstats["build_distances"] * row_bytes + bstats["build_adjacency"] * 2 * a.M * 4,
+        "bstats": bstats, "row_bytes": row_bytes, "gt": gt,
         "build_batches": bstats["build_batches"],
         "at_config_ef": at_cfg,
     }
@@ -363,13 +364,13 @@ def main():
     if world == 1:
         legs = ["single"]
     else:
-        legs = ["shard", "replica"] if a.multi == "both" else [a.multi]
+        legs = ["replica", "shard"] if a.multi == "both" else [a.multi]
     res = {}
     for m in legs:
         if res:  # free the previous leg's HBM before the next build
             res[list(res)[-1]].pop("index", None)
         res[m] = hnsw_leg(c, m)
-    head = res["replica"] if "replica" in res else res[legs[0]]
+    head = res["shard"] if "shard" in res else res[legs[0]]
     replica = head["mode"] == "replica"
     out = {
         "metric": f"kNN QPS @ recall@10>={a.target_recall} (HNSW, {a.rows} x {a.dim} {a.quant} {a.metric})",
@@ -380,8 +381,8 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(head["ms_per_step"], 3),
         "higher_is_better": True,
-        # N=1 is the first point of the replica series the default N>1 run reports
-        "scaling": "weak" if (replica or (world == 1 and a.multi != "shard")) else "strong",
+        # N=1 is the first point of the row-shard series the default N>1 run reports
+        "scaling": "weak" if (replica or (world == 1 and a.multi == "replica")) else "strong",
         "vs_baseline": None,
         "dtype": a.quant,
         "data": f"synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py), "
@@ -405,29 +406,27 @@ def main():
                      "dist_evals_per_query": round(head["dist_per_query"], 1)},
         "build_stats": {"distance_evals_per_vector": round(head["build_dist_per_vector"], 1),
                         "batches": head["build_batches"]},
-        # whole-build wall time (insert + sort + reverse-link launches and host gaps)
-        "build_roofline": {"bound": "hbm",
-                           "achieved": round(head["build_alg_bytes"] / head["build_s"] / 1e9, 1),
-                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(head["build_alg_bytes"] / head["build_s"] / 1e9 / HBM_PEAK_GBS, 4),
-                           "alg_bytes": int(head["build_alg_bytes"])},
+        "build_roofline": build_roofline(a, head),
         "at_config_ef": head["at_config_ef"],
         "f16_traversal_rerank": head.get("f16_rerank"),
         "multi_entry": head.get("multi_entry"),
     }
-    if "shard" in res and head["mode"] != "shard":
-        s = res["shard"]
-        out["shard_mode"] = {"qps": round(s["qps"], 1), "ms_per_step": round(s["ms_per_step"], 3),
-                             "ef": s["ef"], "k_shard": s["k_shard"], "recall_at_10": round(s["recall"], 4),
-                             "build_vectors_per_s": round(s["build_vps"], 1),
-                             "build_seconds": round(s["build_s"], 3),
-                             "kernel_ms": round(s["kern_ms"], 3),
-                             "dist_evals_per_query_per_shard": round(s["dist_per_query"], 1),
-                             "scaling": "strong", "note": "row-range shards, every query searched on every shard",
-                             "at_config_ef": s["at_config_ef"]}
+    if "replica" in res and head["mode"] != "replica":
+        s = res["replica"]
+        out["replica_mode"] = {"qps": round(s["qps"], 1), "ms_per_step": round(s["ms_per_step"], 3),
+                               "ef": s["ef"], "recall_at_10": round(s["recall"], 4),
+                               "build_vectors_per_s": round(s["build_vps"], 1),
+                               "build_seconds": round(s["build_s"], 3),
+                               "kernel_ms": round(s["kern_ms"], 3),
+                               "dist_evals_per_query": round(s["dist_per_query"], 1),
+                               "queries_per_step": a.queries * world,
+                               "scaling": "weak",
+                               "note": "every rank holds the whole index and serves its own query batch",
+                               "at_config_ef": s["at_config_ef"]}
     # CPU baseline (rank 0, N=1 only): oracle/ restatement of usearch
     if world == 1 and rank == 0 and not a.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(a, head["index"], head["q"], head["ef"], head["x"])
+        out["cpu_baseline"] = cpu_baseline(a, head["index"], head["q"], head["ef"], head["x"], head["gt"])
+        out["config"]["cpu_build_sample_rows"] = out["cpu_baseline"]["build_sample_rows"]
         if out["cpu_baseline"].get("qps"):
             out["gpu_over_cpu_qps"] = round(head["qps"] / out["cpu_baseline"]["qps"], 1)
             out["gpu_over_cpu_build"] = round(head["build_vps"] / out["cpu_baseline"]["build_vectors_per_s"], 1)
@@ -520,6 +519,44 @@ def run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_ove
         print(json.dumps(out), flush=True)
 
 
+def build_roofline(a, head):
+    """The build against the HBM roofline on DEVICE time (HIP events around every
+    batch's launches on the build stream, vsg_stats_t.build_*_ns), dominant kernel
+    hnsw_insert_kernel.  Algorithmic bytes of the insert kernel: one row per distance
+    evaluation of the descent and efC beam (distinct nodes of one wave's traversal) +
+    one level-0 adjacency row per expansion.  The heuristic selection's distances are
+    NOT counted: they re-score rows the beam just fetched (the kept set, <= M0 rows,
+    L1/L2-resident), so counting them credited cache hits as HBM bytes (round 1's
+    wall-time model reported 1.04 of peak at C3).  `traffic` = PMC HBM bytes of all
+    insert launches of the build (profiles/build_pmc.json, FETCH_SIZE x2 + WRITE_SIZE)
+    when it matches this workload."""
+    st, rb = head["bstats"], head["row_bytes"]
+    sel = st["build_select_distances"] + st["reverse_select_distances"] + st["reverse_recompute_distances"]
+    beam = st["build_distances"] - sel
+    ins_bytes = beam * rb + st["build_adjacency"] * 2 * a.M * 4
+    rev_bytes = st["reverse_recompute_distances"] * rb
+    t_ins, t_sort, t_rev = (max(1, st[f"build_{k}_ns"]) * 1e-9 for k in ("insert", "sort", "reverse"))
+    ach = ins_bytes / t_ins / 1e9
+    traffic = None
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "build_pmc.json")))
+        w = d.get("workload", {})
+        if (w.get("n"), w.get("dim"), w.get("metric"), w.get("M"), w.get("efc")) == (
+                head["nloc"], a.dim, a.metric, a.M, a.efc):
+            traffic = d.get("insert_hbm_bytes")
+    except (OSError, ValueError):
+        pass
+    return {"bound": "hbm", "kernel": "hnsw_insert_kernel", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_unit": "HBM bytes over all insert launches of the build",
+            "alg_bytes_insert": int(ins_bytes),
+            "kernel_s": {"insert": round(t_ins, 4), "sort": round(t_sort, 4), "reverse": round(t_rev, 4)},
+            "reverse_achieved_gbs": round(rev_bytes / t_rev / 1e9, 1),
+            "wall_s": round(head["build_s"], 4),
+            "beam_distance_evals_per_vector": round(beam / max(1, head["nloc"]), 1),
+            "selection_distance_evals_per_vector": round(sel / max(1, head["nloc"]), 1)}
+
+
 def pmc_traffic(a, ef):
     """HBM bytes per search launch from the committed rocprofv3 PMC summary
     (profiles/search_pmc.json, written by tools/pmc_summary.py from separate
@@ -567,13 +604,13 @@ def host_cores() -> int:
     return max(1, n)
 
 
-def cpu_baseline(a, index, q_t, ef, x_t):
+def cpu_baseline(a, index, q_t, ef, x_t, gt):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # the checker / CPU baseline only (never the product path)
 
     O.set_fast_metric(True)
     threads = host_cores()
-    res = {"unit": "queries/s", "cores": threads, "kind": "port", "cpu": cpu_model()}
+    res = {"unit": "queries/s", "cores": threads, "kind": "port", "cpu": cpu_model(), "isa": O.fast_isa()}
     # (1) search QPS: the same graph, exported from HBM, searched by the C restatement
     g = index.export()
     h = O.HnswOracle(a.dim, a.metric, a.M, a.efc, ef)
@@ -586,10 +623,15 @@ def cpu_baseline(a, index, q_t, ef, x_t):
     dt = time.perf_counter() - t0
     n2 = int(min(len(qh), max(n, n * a.cpu_seconds / max(dt, 1e-6))))
     t0 = time.perf_counter()
-    h.search(qh[:n2], a.k, ef, threads=threads)
+    ck = h.search(qh[:n2], a.k, ef, threads=threads)[0]
     dt = time.perf_counter() - t0
     res["value"] = round(n2 / dt, 1)
     res["qps"] = res["value"]
+    # the CPU's recall at the matched ef (the bench queries' first rows are the
+    # ground-truth queries): equal to the GPU's up to near-ties on the same graph
+    ng = min(n2, gt.shape[0])
+    res["recall_at_10"] = round(float(np.mean([len(set(ck[i].astype(np.int64)) & set(gt[i])) / a.k for i in range(ng)])), 4)
+    res["ef"] = ef
     del h
     # (2) build vectors/s: concurrent inserts into a fresh index, bounded sample
     xh = x_t[: 200_000].cpu().numpy()
@@ -604,9 +646,11 @@ def cpu_baseline(a, index, q_t, ef, x_t):
     hb2.add(np.arange(nb2), xh[:nb2], threads=threads)
     dt = time.perf_counter() - t0
     res["build_vectors_per_s"] = round(nb2 / dt, 1)
-    res["sample"] = (f"search: {n2} queries at ef={ef} over the GPU-built 1M-row graph exported to host; "
-                     f"build: {nb2} inserts into a fresh index (efC={a.efc}, M={a.M}); "
-                     f"{threads} threads, SIMD f32 metrics")
+    res["build_sample_rows"] = nb2
+    res["sample"] = (f"search: {n2} queries at ef={ef} over the GPU-built {a.rows}-row graph exported to host "
+                     f"(recall on the first {ng}); build: {nb2} inserts into a fresh index (efC={a.efc}, "
+                     f"M={a.M}) -- a bounded sample, not the full {a.rows} rows; {threads} threads, "
+                     f"{O.fast_isa()} f32 metrics")
     return res
 
 

@@ -89,6 +89,9 @@ typedef struct {
     uint64_t reverse_select_distances; /* reverse links: heuristic re-selection */
     uint64_t reverse_prunes;           /* (level, node) segments that overflowed and were re-selected */
     uint64_t reverse_appends;          /* segments appended without re-selection */
+    uint64_t build_insert_ns;          /* device time of the build kernels (HIP events on the build */
+    uint64_t build_sort_ns;            /*   stream): insert (descent + beam + selection), pair sort, */
+    uint64_t build_reverse_ns;         /*   reverse links -- the build roofline's time base */
 } vsg_stats_t;
 
 /* replaces usearch::Index::new(&options) — src/index/usearch.rs:98 */

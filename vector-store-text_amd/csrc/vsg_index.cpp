@@ -168,6 +168,10 @@ struct vsg_index {
     uint32_t entry = 0xFFFFFFFFu;
     int max_level = -1;
     std::atomic<uint64_t> build_vectors{0}, build_batches{0};
+    // device time of the build kernels (writer side): events recorded around each
+    // batch's insert / sort / reverse launches, read after the call's final sync
+    std::vector<hipEvent_t> ev_pool;
+    uint64_t t_insert_ns = 0, t_sort_ns = 0, t_reverse_ns = 0;
 
     // build workspace (writer side only)
     int8_t* d_blevels = nullptr;
@@ -205,6 +209,8 @@ struct vsg_index {
 };
 
 static void free_dev(vsg_index* h) {
+    for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    h->ev_pool.clear();
     for (SearchCtx* c : h->ctx_free) delete c;
     h->ctx_free.clear();
     for (Workspace* w : h->ws_free) delete w;
@@ -391,6 +397,17 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
     HIP_TRY(hipMemcpyAsync(h->d_bnodes, order.data(), n * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_blevels, blev.data(), n, hipMemcpyHostToDevice, st));
 
+    size_t nev = 0;  // events used from the pool: 4 per batch
+    auto next_ev = [&](hipEvent_t* e) -> hipError_t {
+        if (nev == h->ev_pool.size()) {
+            hipEvent_t x;
+            const hipError_t r = hipEventCreate(&x);
+            if (r != hipSuccess) return r;
+            h->ev_pool.push_back(x);
+        }
+        *e = h->ev_pool[nev++];
+        return hipSuccess;
+    };
     const double frac = env_double("VSG_BUILD_BATCH_FRAC", 1.0 / 16.0);
     // probe knobs: a second batch fraction once the graph holds `switch_at` nodes
     const double frac2 = env_double("VSG_BUILD_BATCH_FRAC2", frac);
@@ -444,7 +461,14 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
         ip.efc = h->efc;
         ip.hash_size = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", 16));
         ip.stats = h->d_stats;
+        hipEvent_t e0, e1, e2, e3;
+        HIP_TRY(next_ev(&e0));
+        HIP_TRY(next_ev(&e1));
+        HIP_TRY(next_ev(&e2));
+        HIP_TRY(next_ev(&e3));
+        HIP_TRY(hipEventRecord(e0, st));
         HIP_TRY(launch_insert(h->st, h->mk, ip, st));
+        HIP_TRY(hipEventRecord(e1, st));
 
         size_t tmp = 0;
         HIP_TRY(sort_pairs(nullptr, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], npairs, st));
@@ -456,6 +480,7 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
         }
         tmp = h->sort_tmp_bytes;
         HIP_TRY(sort_pairs(h->d_sort_tmp, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], npairs, st));
+        HIP_TRY(hipEventRecord(e2, st));
 
         ReverseParams rp{};
         rp.g = h->graph();
@@ -469,6 +494,7 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
         const size_t ppw = std::max<size_t>(1, (size_t)env_double("VSG_REVERSE_PAIRS_PER_WAVE", 16));
         const int grid = (int)std::max<size_t>(1, std::min<size_t>(rgrid, (npairs + ppw - 1) / ppw));
         HIP_TRY(launch_reverse(h->st, h->mk, rp, grid, st));
+        HIP_TRY(hipEventRecord(e3, st));
 
         if (new_top >= 0) {
             h->entry = order[i + b - 1];
@@ -478,6 +504,16 @@ static int insert_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* key
         i += b;
     }
     h->build_vectors += n;
+    if (nev) {
+        HIP_TRY(hipStreamSynchronize(st));
+        for (size_t b = 0; b + 3 < nev; b += 4) {
+            float t[3] = {0.f, 0.f, 0.f};
+            for (int j = 0; j < 3; ++j) HIP_TRY(hipEventElapsedTime(&t[j], h->ev_pool[b + j], h->ev_pool[b + j + 1]));
+            h->t_insert_ns += (uint64_t)(t[0] * 1e6);
+            h->t_sort_ns += (uint64_t)(t[1] * 1e6);
+            h->t_reverse_ns += (uint64_t)(t[2] * 1e6);
+        }
+    }
     return VSG_OK;
 }
 
@@ -1197,6 +1233,9 @@ int vsg_index_stats(const vsg_index_t* h, vsg_stats_t* out) {
     out->reverse_select_distances = s[7];
     out->reverse_prunes = s[8];
     out->reverse_appends = s[9];
+    out->build_insert_ns = h->t_insert_ns;
+    out->build_sort_ns = h->t_sort_ns;
+    out->build_reverse_ns = h->t_reverse_ns;
     return VSG_OK;
 }
 
@@ -1215,6 +1254,7 @@ int vsg_index_reset_stats(vsg_index_t* h) {
     HIP_TRY(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
     h->build_vectors = 0;
     h->build_batches = 0;
+    h->t_insert_ns = h->t_sort_ns = h->t_reverse_ns = 0;
     return VSG_OK;
 }
 

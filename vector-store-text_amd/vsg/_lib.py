@@ -65,6 +65,9 @@ class Stats(C.Structure):
         ("reverse_select_distances", C.c_uint64),
         ("reverse_prunes", C.c_uint64),
         ("reverse_appends", C.c_uint64),
+        ("build_insert_ns", C.c_uint64),
+        ("build_sort_ns", C.c_uint64),
+        ("build_reverse_ns", C.c_uint64),
     ]
 
 

@@ -1,0 +1,108 @@
+"""GPU: BASELINE.json configs C3 and C5 at full size (VERDICT r1 missing/weak #4).
+
+C3 (configs[2]): 10M x 768 f32 cosine, index row-sharded x 8 with a top-k merge.  On
+one GPU the 8 shards are built one after another (the 8-GPU run is the driver's); each
+shard is an independent HNSW graph over rows [s N/8, (s+1) N/8) with its own level seed,
+exactly the per-rank index of bench.py's shard leg.  Every query is searched on every
+shard and the per-shard top-k rows are merged by the HIP merge kernel (the step after
+the RCCL all-gather).  Checks: merged exact top-k == one exact-only index over all 10M
+rows (bit-exact keys and distances); merged HNSW recall@10 >= 0.95 at the per-shard ef
+the 8-shard emulation needs (32, profiles/r01_c3_8shard_emulation_1gpu*.jsonl).
+
+C5 (configs[4]): 1M x 1536 f32 inner product, batched brute force on the f32 matrix
+cores (mfma_exact.hip, `v_mfma_f32_32x32x2_f32`).  Bit-exact against the oracle at
+1536-d on integer data; at full size MFMA == VALU exact kernel up to near-ties.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import vsg
+from vsg import datagen as G
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
+
+
+def recall(found, truth, k):
+    return float(np.mean([len(set(found[i][:k].tolist()) & set(truth[i][:k].tolist())) / k
+                          for i in range(truth.shape[0])]))
+
+
+def test_c3_10m768_cos_eight_row_shards_merged():
+    import torch
+    n, dim, shards, nq, k = 10_000_000, 768, 8, 1000, 10
+    bs, qs, ms = G.config_seeds(2)
+    q = vsg.datagen_device("clustered", nq, dim, qs, ms)
+    full = vsg.Index(dim, "cos", "f32", exact_only=True)
+    full.reserve(n)
+    parts = []
+    for s in range(shards):
+        lo, hi = s * n // shards, (s + 1) * n // shards
+        x = vsg.datagen_device("clustered", hi - lo, dim, bs, ms, start=lo)
+        idx = vsg.Index(dim, "cos", "f32", 16, 128, 64, seed=0x5EED + s)
+        idx.reserve(hi - lo)
+        keys = np.arange(lo, hi, dtype=np.uint64)
+        idx.add_device(keys, x)
+        full.add_device(keys, x)
+        torch.cuda.synchronize()
+        del x
+        parts.append(idx)
+    assert sum(p.size() for p in parts) == n and full.size() == n
+
+    def merged(ef, exact=False):
+        outs = [p.search_device(q, k, ef, exact=exact) for p in parts]
+        mk, md = vsg.merge_topk_device(torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs]), k)
+        return mk.cpu().numpy().view(np.uint64), md.cpu().numpy()
+
+    ek, ed = merged(0, exact=True)
+    tk, td = full.search_device(q, k, exact=True)
+    np.testing.assert_array_equal(ek, tk.cpu().numpy().view(np.uint64))
+    np.testing.assert_array_equal(ed, td.cpu().numpy())
+    r = {ef: recall(merged(ef)[0], ek, k) for ef in (16, 32, 64)}
+    print("C3 8-shard merged recall@10 by per-shard ef:", r)
+    assert r[32] >= 0.95 and r[64] >= r[32] - 0.002
+
+
+def test_c5_1536_ip_mfma_bitexact_vs_oracle(monkeypatch):
+    n, dim, nq, k = 5000, 1536, 160, 10
+    x = np.floor(G.uint8_valued(n, dim, 51) / 16.0)   # sums < 2^24: exact in f32
+    q = np.floor(G.uint8_valued(nq, dim, 52) / 16.0)
+    keys = np.arange(n, dtype=np.uint64) * 5 + 2
+    idx = vsg.Index(dim, "ip", "f32", exact_only=True)
+    idx.add(keys, x)
+    idx.remove(keys[::9])
+    removed = np.zeros(n, np.uint8)
+    removed[::9] = 1
+    ok, od, oc = O.exact_search("ip", x, q, k, keys=keys, removed=removed)
+    for mfma in ("1", "0"):
+        monkeypatch.setenv("VSG_EXACT_MFMA", mfma)
+        m = idx.exact_search(q, k)
+        np.testing.assert_array_equal(m.keys, ok)
+        np.testing.assert_array_equal(m.distances, od)
+        np.testing.assert_array_equal(m.counts, oc)
+
+
+def test_c5_1m1536_ip_mfma_vs_valu_full_size(monkeypatch):
+    import torch
+    n, dim, nq, k = 1_000_000, 1536, 256, 10
+    bs, qs, ms = G.config_seeds(4)
+    x = vsg.datagen_device("clustered", n, dim, bs, ms)
+    q = vsg.datagen_device("clustered", nq, dim, qs, ms)
+    idx = vsg.Index(dim, "ip", "f32", exact_only=True)
+    idx.reserve(n)
+    idx.add_device(np.arange(n, dtype=np.uint64), x)
+    del x
+    res = {}
+    for mfma in ("1", "0"):
+        monkeypatch.setenv("VSG_EXACT_MFMA", mfma)
+        kk, dd = idx.search_device(q, k + 1, exact=True)
+        torch.cuda.synchronize()
+        res[mfma] = (kk.cpu().numpy().view(np.uint64), dd.cpu().numpy())
+    (mk, md), (vk, vd) = res["1"], res["0"]
+    scale = np.maximum(1.0, np.abs(vd))
+    assert np.max(np.abs(md - vd) / scale) < 1e-5
+    same = np.all(mk[:, :k] == vk[:, :k], axis=1)
+    for i in np.flatnonzero(~same):  # a differing row sits on a near-tie among the top k + 1
+        assert np.min(np.diff(vd[i])) / scale[i].max() < 1e-5 or set(mk[i, :k]) == set(vk[i, :k]), i
+    assert same.mean() >= 0.98
+    assert np.all(np.diff(md[:, :k], axis=1) >= 0)

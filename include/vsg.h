@@ -17,9 +17,14 @@
  * for the last failing call on this thread (the host shim maps it to
  * anyhow!, like src/index/usearch.rs:259-272, :281-295).
  *
- * Threading: add/remove/reserve serialise on an index-wide writer lock (the
- * reference's RwLock write side, usearch.rs:201-212); search/exact_search take
- * the shared side and may run concurrently with each other.
+ * Threading: every call is thread-safe.  Writers (add/remove/reserve/compact/
+ * import) serialise among themselves.  Searches may run concurrently with each
+ * other AND with an add (the reference runs add and search together under its
+ * RwLock read side and usearch's own thread safety, usearch.rs:201-221, 276):
+ * an add holds the index-wide lock only to stage its slots and to publish them,
+ * not while the graph is built, so a search issued during a long batched build
+ * answers at once from the last completed state (plus any rows of the build in
+ * flight it reaches through new links -- a prefix of the writes).
  */
 #ifndef VSG_H
 #define VSG_H
@@ -237,7 +242,9 @@ typedef struct {
     uint32_t max_wait_us;       /* optional coalescing window; 0 => natural batching */
     uint32_t compact_percent;   /* vsg_index_compact once tombstones >= this % of stored
                                    rows; 0 => 50, >= 100 => never */
-    uint32_t reserved;
+    uint32_t concurrent_reads;  /* 1: anns run on a second worker beside the writes and see a
+                                   prefix of them (the reference's fire-and-forget adds,
+                                   usearch.rs:200-221); 0: submission order (default) */
     uint64_t compact_min_dead;  /* ... and at least this many; 0 => 4096 */
 } vsg_actor_options_t;
 
@@ -266,7 +273,8 @@ int vsg_actor_ann(vsg_actor_t* actor, const float* embedding, size_t dims, size_
                   uint64_t* out_keys, float* out_distances, size_t* out_count);
 /* Index::Count — usearch.rs:308-311 (live size) */
 int vsg_actor_count(vsg_actor_t* actor, size_t* out);
-/* wait until all previously submitted messages are applied */
+/* wait until all previously submitted writes (and, in submission-order mode,
+ * every other message) are applied */
 int vsg_actor_flush(vsg_actor_t* actor);
 int vsg_actor_counters(const vsg_actor_t* actor, vsg_actor_counters_t* out);
 /* borrowed handle of the actor's index (stats, export); valid until vsg_actor_free */

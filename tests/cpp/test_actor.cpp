@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <map>
 #include <random>
+#include <shared_mutex>
 #include <thread>
 
 #include "../../vector-store-text_amd/csrc/actor.hpp"
@@ -314,7 +315,99 @@ static void test_auto_compaction() {
     CHECK(b.flush() == 0 && m2->compactions == 0 && m2->stored == 1000);
 }
 
+// 6) concurrent_reads: a backend shaped like vsg_index (an add builds for a long
+//    time with no lock held, then publishes its rows under the exclusive lock;
+//    searches take the shared side).  An Ann issued during a 300 ms add answers
+//    long before the add ends, from a prefix of the writes; in the default mode
+//    the same Ann waits for the add (submission order).
+struct ConcMock final : vsg::ActorBackend {
+    mutable std::shared_mutex mu;
+    std::map<uint64_t, float> rows;  // key -> 1-d value
+    size_t cap = 0;
+    std::atomic<int> adds_in_flight{0};
+    size_t dimensions() const override { return 1; }
+    size_t size() const override {
+        std::shared_lock<std::shared_mutex> lk(mu);
+        return rows.size();
+    }
+    size_t capacity() const override { return cap; }
+    size_t expansion_search() const override { return 16; }
+    bool contains(uint64_t k) const override {
+        std::shared_lock<std::shared_mutex> lk(mu);
+        return rows.count(k) != 0;
+    }
+    int reserve(size_t c) override {
+        cap = std::max(cap, c);
+        return 0;
+    }
+    int add(const uint64_t* k, const float* v, size_t n) override {
+        adds_in_flight++;
+        std::this_thread::sleep_for(std::chrono::milliseconds(300));  // the batched build
+        std::unique_lock<std::shared_mutex> lk(mu);                    // publish
+        for (size_t i = 0; i < n; ++i) rows[k[i]] = v[i];
+        adds_in_flight--;
+        return 0;
+    }
+    int remove(const uint64_t* k, size_t n, size_t* r) override {
+        std::unique_lock<std::shared_mutex> lk(mu);
+        size_t c = 0;
+        for (size_t i = 0; i < n; ++i) c += rows.erase(k[i]);
+        if (r) *r = c;
+        return 0;
+    }
+    int search(const float* q, size_t nq, size_t k, size_t, uint64_t* keys, float* dist,
+               size_t* counts) override {
+        std::shared_lock<std::shared_mutex> lk(mu);
+        for (size_t i = 0; i < nq; ++i) {
+            std::vector<std::pair<float, uint64_t>> all;
+            for (auto& kv : rows) all.push_back({(kv.second - q[i]) * (kv.second - q[i]), kv.first});
+            std::sort(all.begin(), all.end());
+            const size_t c = std::min(k, all.size());
+            for (size_t j = 0; j < k; ++j) {
+                keys[i * k + j] = j < c ? all[j].second : ~0ull;
+                dist[i * k + j] = j < c ? all[j].first : INFINITY;
+            }
+            counts[i] = c;
+        }
+        return 0;
+    }
+};
+
+static void test_concurrent_reads_beside_writes() {
+    for (int concurrent = 1; concurrent >= 0; --concurrent) {
+        auto* m = new ConcMock;
+        ConcMock* mp = m;
+        vsg::ActorConfig cfg;
+        cfg.reserve_increment = 1000;
+        cfg.concurrent_reads = concurrent != 0;
+        vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), cfg);
+        CHECK(a.init() == 0);
+        const float v1 = 1.f, v2 = 2.f;
+        a.add_or_replace(1, &v1);
+        CHECK(a.flush() == 0);
+        a.add_or_replace(2, &v2);  // a 300 ms "build"
+        while (mp->adds_in_flight.load() == 0) std::this_thread::sleep_for(std::chrono::microseconds(100));
+        uint64_t keys[2];
+        float dist[2];
+        size_t cnt = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        CHECK(a.ann(&v2, 1, 2, keys, dist, &cnt) == 0);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (concurrent) {
+            CHECK(ms < 150.0);                              // answered during the build
+            CHECK(cnt == 1 && keys[0] == 1);                // the prefix before the add
+            CHECK(mp->adds_in_flight.load() == 1);
+        } else {
+            CHECK(ms > 150.0);                              // waited for the add (FIFO)
+            CHECK(cnt == 2 && keys[0] == 2 && keys[1] == 1);
+        }
+        CHECK(a.flush() == 0);
+        CHECK(a.ann(&v2, 1, 2, keys, dist, &cnt) == 0 && cnt == 2 && keys[0] == 2);
+    }
+}
+
 int main() {
+    test_concurrent_reads_beside_writes();
     test_fifo_semantics();
     test_concurrent_anns();
     test_ef_groups_and_errors();

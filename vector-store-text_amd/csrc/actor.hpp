@@ -12,11 +12,16 @@
 //   * add/remove failures are swallowed (counted here, logged there) :207-224, :246
 //   * ann dimension checks before any search                       :259-272
 //   * count = live size                                            :308-311
-// Ordering is stronger than the reference's (which spawns every message as
-// its own task): messages are applied in submission order, so an Ann sees every
-// write submitted before it.  Batching never changes a result: an Ann run is
-// split by effective ef = max(ef, k) and a query's top-k is the prefix of its
-// group's top-kmax (the search returns the first k live entries of its list).
+// Ordering, default: stronger than the reference's (which spawns every message
+// as its own task): messages are applied in submission order, so an Ann sees
+// every write submitted before it.  With concurrent_reads, Anns go to a second
+// worker that searches while the writer builds (the reference's behaviour:
+// add is fire-and-forget on rayon, search runs beside it under the shared lock,
+// usearch.rs:200-221, :274-277): an Ann then sees a prefix of the writes, and a
+// burst of inserts no longer delays queries by the whole batched build.
+// Batching never changes a result: an Ann run is split by effective ef =
+// max(ef, k) and a query's top-k is the prefix of its group's top-kmax (the
+// search returns the first k live entries of its list).
 #pragma once
 #include <algorithm>
 #include <chrono>
@@ -67,6 +72,9 @@ struct ActorConfig {
     // as a tombstone (usearch.rs:214-221), so an upsert stream needs this.
     uint32_t compact_percent = 50;
     size_t compact_min_dead = 4096;
+    // Anns on their own worker, beside the writes (needs a backend whose search
+    // may run concurrently with add/remove, as vsg_index's does)
+    bool concurrent_reads = false;
 };
 
 struct ActorCounters {
@@ -114,7 +122,8 @@ class Actor {
 
     Actor(std::unique_ptr<ActorBackend> be, const ActorConfig& cfg) : be_(std::move(be)), cfg_(cfg) {
         if (cfg_.max_batch == 0) cfg_.max_batch = 1;
-        worker_ = std::thread([this] { run(); });
+        worker_ = std::thread([this] { run(q_, qcv_); });
+        if (cfg_.concurrent_reads) reader_ = std::thread([this] { run(rq_, rcv_); });
     }
 
     ~Actor() {
@@ -123,7 +132,9 @@ class Actor {
             stop_ = true;
         }
         qcv_.notify_all();
+        rcv_.notify_all();
         worker_.join();
+        if (reader_.joinable()) reader_.join();
     }
 
     // initial reservation, usearch.rs:99
@@ -197,30 +208,33 @@ class Actor {
 
   private:
     void push(Msg&& m) {
+        const bool read = cfg_.concurrent_reads && m.kind == ANN;
         {
             std::lock_guard<std::mutex> lk(qm_);
-            q_.push_back(std::move(m));
+            (read ? rq_ : q_).push_back(std::move(m));
         }
-        qcv_.notify_one();
+        (read ? rcv_ : qcv_).notify_one();
     }
 
-    void run() {
+    // one worker: the FIFO of writes (and, by default, everything else), or the
+    // Ann queue of concurrent_reads; both share qm_
+    void run(std::deque<Msg>& q, std::condition_variable& cv) {
         std::vector<Msg> batch;
         for (;;) {
             {
                 std::unique_lock<std::mutex> lk(qm_);
-                qcv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-                if (q_.empty() && stop_) return;
-                if (cfg_.max_wait_us && q_.size() < cfg_.max_batch && !stop_) {
-                    qcv_.wait_for(lk, std::chrono::microseconds(cfg_.max_wait_us),
-                                  [&] { return stop_ || q_.size() >= cfg_.max_batch; });
+                cv.wait(lk, [&] { return stop_ || !q.empty(); });
+                if (q.empty() && stop_) return;
+                if (cfg_.max_wait_us && q.size() < cfg_.max_batch && !stop_) {
+                    cv.wait_for(lk, std::chrono::microseconds(cfg_.max_wait_us),
+                                [&] { return stop_ || q.size() >= cfg_.max_batch; });
                 }
-                const size_t n = std::min(q_.size(), cfg_.max_batch);
+                const size_t n = std::min(q.size(), cfg_.max_batch);
                 batch.clear();
                 batch.reserve(n);
                 for (size_t i = 0; i < n; ++i) {
-                    batch.push_back(std::move(q_.front()));
-                    q_.pop_front();
+                    batch.push_back(std::move(q.front()));
+                    q.pop_front();
                 }
             }
             process(batch);
@@ -397,12 +411,12 @@ class Actor {
     std::unique_ptr<ActorBackend> be_;
     ActorConfig cfg_;
     std::mutex qm_;
-    std::condition_variable qcv_;
-    std::deque<Msg> q_;
+    std::condition_variable qcv_, rcv_;
+    std::deque<Msg> q_, rq_;
     bool stop_ = false;
     mutable std::mutex cm_;
     ActorCounters ctr_;
-    std::thread worker_;
+    std::thread worker_, reader_;
 };
 
 }  // namespace vsg

@@ -65,6 +65,7 @@ int vsg_actor_new(const vsg_actor_options_t* o, vsg_actor_t** out) {
     cfg.max_wait_us = o->max_wait_us;
     if (o->compact_percent) cfg.compact_percent = o->compact_percent;
     if (o->compact_min_dead) cfg.compact_min_dead = o->compact_min_dead;
+    cfg.concurrent_reads = o->concurrent_reads != 0;
     const size_t ef = o->index.expansion_search ? o->index.expansion_search : 64;
     auto* a = new vsg_actor;
     a->index = h;

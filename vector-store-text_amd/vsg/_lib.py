@@ -91,7 +91,7 @@ class ActorOptions(C.Structure):
         ("max_batch", C.c_uint32),
         ("max_wait_us", C.c_uint32),
         ("compact_percent", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("concurrent_reads", C.c_uint32),
         ("compact_min_dead", C.c_uint64),
     ]
 

@@ -51,9 +51,10 @@ def test_search_during_a_large_add():
         done.set()
 
     th = threading.Thread(target=writer)
+    t_start = time.perf_counter()
     th.start()
     time.sleep(0.05)
-    lat, results = [], []
+    lat, results, slow = [], [], []
     while not done.is_set():
         t0 = time.perf_counter()
         m = idx.search(q, 10, 64)
@@ -61,7 +62,10 @@ def test_search_during_a_large_add():
         if not done.is_set():
             lat.append(dt)
             results.append(m)
+            if dt > 0.02:
+                slow.append((round(t0 - t_start, 3), round(dt, 3)))
     th.join()
+    print("slow searches (start s, latency s):", slow)
     xh = xt.cpu().numpy()
     print(f"add {t_add['s']:.3f} s; {len(lat)} searches during it, max latency {max(lat or [0]) * 1e3:.1f} ms")
     assert len(lat) >= 3, "searches must not wait for the whole build"
@@ -107,7 +111,8 @@ def test_actor_concurrent_reads_mode():
     """vsg.Actor(concurrent_reads=True): Anns on their own worker beside a write run."""
     dim = 64
     x = G.uint8_valued(300_000, dim, 77)
-    a = vsg.Actor(dim, "l2sq", "f32", 16, 128, 64, reserve_increment=400_000, concurrent_reads=True,
+    from vsg.actor import Actor
+    a = Actor(dim, "l2sq", "f32", 16, 128, 64, reserve_increment=400_000, concurrent_reads=True,
                   max_batch=400_000)
     for i in range(1000):
         a.add_or_replace(i, x[i])

@@ -421,19 +421,15 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         order[i] += s0;
         blev[i] = h->h_levels[order[i]];
     }
-    HIP_TRY(hipMemcpyAsync(h->d_bnodes, order.data(), n * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(h->d_blevels, blev.data(), n, hipMemcpyHostToDevice, st));
-
-    size_t nev = 0;  // events used from the pool: 4 per batch
-    auto next_ev = [&](hipEvent_t* e) -> hipError_t {
-        if (nev == h->ev_pool.size()) {
-            hipEvent_t x;
-            const hipError_t r = hipEventCreate(&x);
-            if (r != hipSuccess) return r;
-            h->ev_pool.push_back(x);
-        }
-        *e = h->ev_pool[nev++];
-        return hipSuccess;
+    // Plan the whole call on the host first (batch boundaries, entry-point
+    // changes, pair offsets), then size every buffer once: no allocation -- and
+    // so no device-wide synchronisation -- between the launches, which run
+    // beside concurrent searches.
+    struct Batch {
+        size_t i, b, npairs;
+        uint32_t entry;  // entry point / top level the batch descends from
+        int max_level;
+        int new_top;  // > max_level: the batch's last node becomes the entry
     };
     const double frac = env_double("VSG_BUILD_BATCH_FRAC", 1.0 / 16.0);
     // probe knobs: a second batch fraction once the graph holds `switch_at` nodes
@@ -442,100 +438,126 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 32768);
     // at least 8 batches per call, so the call's own nodes find each other
     const size_t bcall = std::max<size_t>(1, n / 8);
-    std::vector<uint32_t> pair_off(n + 1);
-
-    size_t i = 0;
-    if (h->entry == 0xFFFFFFFFu) {
-        h->entry = order[0];
-        h->max_level = blev[0];
-        i = 1;
-    }
-    while (i < n) {
-        const size_t graph_nodes = (size_t)h->slots - n + i;
-        size_t b = (size_t)std::floor((double)graph_nodes * (switch_at > 0 && graph_nodes >= switch_at ? frac2 : frac));
-        b = std::max<size_t>(1, std::min(std::min(b, bmax), bcall));
-        b = std::min(b, n - i);
-        int new_top = -1;
-        for (size_t j = i; j < i + b; ++j) {
-            if (blev[j] > h->max_level) {
-                b = j - i + 1;
-                new_top = blev[j];
-                break;
+    std::vector<uint32_t> pair_off(n);
+    std::vector<Batch> plan;
+    size_t max_pairs = 0;
+    {
+        uint32_t entry = h->entry;
+        int maxl = h->max_level;
+        size_t i = 0;
+        if (entry == 0xFFFFFFFFu) {
+            entry = order[0];
+            maxl = blev[0];
+            pair_off[0] = 0;
+            i = 1;
+        }
+        while (i < n) {
+            const size_t graph_nodes = (size_t)h->slots - n + i;
+            size_t b = (size_t)std::floor((double)graph_nodes *
+                                          (switch_at > 0 && graph_nodes >= switch_at ? frac2 : frac));
+            b = std::max<size_t>(1, std::min(std::min(b, bmax), bcall));
+            b = std::min(b, n - i);
+            int new_top = -1;
+            for (size_t j = i; j < i + b; ++j) {
+                if (blev[j] > maxl) {
+                    b = j - i + 1;
+                    new_top = blev[j];
+                    break;
+                }
             }
+            // pair offsets: each node emits <= M0 + min(L, maxl) * M pairs
+            uint32_t acc = 0;
+            for (size_t j = 0; j < b; ++j) {
+                pair_off[i + j] = acc;
+                acc += (uint32_t)(h->M0 + std::min<int>(blev[i + j], maxl) * h->M);
+            }
+            plan.push_back({i, b, (size_t)acc, entry, maxl, new_top});
+            max_pairs = std::max<size_t>(max_pairs, acc);
+            if (new_top >= 0) {
+                entry = order[i + b - 1];
+                maxl = new_top;
+            }
+            i += b;
         }
-        // pair offsets: each node emits <= M0 + min(L, maxl) * M pairs
-        uint32_t acc = 0;
-        for (size_t j = 0; j < b; ++j) {
-            pair_off[i + j] = acc;
-            const int L = std::min<int>(blev[i + j], h->max_level);
-            acc += (uint32_t)(h->M0 + L * h->M);
+        if (plan.empty()) {  // a single node into an empty graph
+            h->entry = entry;
+            h->max_level = maxl;
         }
-        const size_t npairs = acc;
-        if ((rc = ensure_pairs(h, npairs))) return rc;
-        HIP_TRY(hipMemcpyAsync(h->d_pair_off + i, pair_off.data() + i, b * 4, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemsetAsync(h->d_pk[0], 0xFF, npairs * 8, st));
-
-        InsertParams ip{};
-        ip.g = h->graph();
-        ip.nodes = h->d_bnodes + i;
-        ip.nnodes = (int)b;
-        ip.levels = h->d_blevels + i;
-        ip.pair_off = h->d_pair_off + i;
-        ip.pair_keys = h->d_pk[0];
-        ip.pair_vals = h->d_pv[0];
-        ip.entry = h->entry;
-        ip.max_level = h->max_level;
-        ip.efc = h->efc;
-        ip.hash_size = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", 16));
-        ip.stats = h->d_stats;
-        hipEvent_t e0, e1, e2, e3;
-        HIP_TRY(next_ev(&e0));
-        HIP_TRY(next_ev(&e1));
-        HIP_TRY(next_ev(&e2));
-        HIP_TRY(next_ev(&e3));
-        HIP_TRY(hipEventRecord(e0, st));
-        HIP_TRY(launch_insert(h->st, h->mk, ip, st));
-        HIP_TRY(hipEventRecord(e1, st));
-
+    }
+    if ((rc = ensure_pairs(h, max_pairs))) return rc;
+    {
         size_t tmp = 0;
-        HIP_TRY(sort_pairs(nullptr, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], npairs, st));
+        HIP_TRY(sort_pairs(nullptr, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], max_pairs, st));
         if (tmp > h->sort_tmp_bytes) {
             hipFree(h->d_sort_tmp);
             h->d_sort_tmp = nullptr;
+            h->sort_tmp_bytes = 0;
             HIP_TRY(hipMalloc(&h->d_sort_tmp, tmp * 2));
             h->sort_tmp_bytes = tmp * 2;
         }
-        tmp = h->sort_tmp_bytes;
-        HIP_TRY(sort_pairs(h->d_sort_tmp, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], npairs, st));
-        HIP_TRY(hipEventRecord(e2, st));
+    }
+    while (h->ev_pool.size() < 4 * plan.size()) {  // device time of every launch
+        hipEvent_t x;
+        HIP_TRY(hipEventCreate(&x));
+        h->ev_pool.push_back(x);
+    }
+    HIP_TRY(hipMemcpyAsync(h->d_bnodes, order.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_blevels, blev.data(), n, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_pair_off, pair_off.data(), n * 4, hipMemcpyHostToDevice, st));
 
+    // a few pairs per wave: the cost is in the few segments that need a
+    // heuristic re-selection, so spread them over as many waves as possible
+    const size_t rgrid = (size_t)env_double("VSG_REVERSE_GRID", (double)h->reverse_grid);
+    const size_t ppw = std::max<size_t>(1, (size_t)env_double("VSG_REVERSE_PAIRS_PER_WAVE", 16));
+    const int hash = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", 16));
+    for (size_t bi = 0; bi < plan.size(); ++bi) {
+        const Batch& B = plan[bi];
+        hipEvent_t* ev = &h->ev_pool[4 * bi];
+        HIP_TRY(hipMemsetAsync(h->d_pk[0], 0xFF, B.npairs * 8, st));
+        InsertParams ip{};
+        ip.g = h->graph();
+        ip.nodes = h->d_bnodes + B.i;
+        ip.nnodes = (int)B.b;
+        ip.levels = h->d_blevels + B.i;
+        ip.pair_off = h->d_pair_off + B.i;
+        ip.pair_keys = h->d_pk[0];
+        ip.pair_vals = h->d_pv[0];
+        ip.entry = B.entry;
+        ip.max_level = B.max_level;
+        ip.efc = h->efc;
+        ip.hash_size = hash;
+        ip.stats = h->d_stats;
+        HIP_TRY(hipEventRecord(ev[0], st));
+        HIP_TRY(launch_insert(h->st, h->mk, ip, st));
+        HIP_TRY(hipEventRecord(ev[1], st));
+        size_t tmp = h->sort_tmp_bytes;
+        HIP_TRY(sort_pairs(h->d_sort_tmp, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], B.npairs, st));
+        HIP_TRY(hipEventRecord(ev[2], st));
         ReverseParams rp{};
         rp.g = h->graph();
         rp.keys = h->d_pk[1];
         rp.vals = h->d_pv[1];
-        rp.npairs = npairs;
+        rp.npairs = B.npairs;
         rp.stats = h->d_stats;
-        // a few pairs per wave: the cost is in the few segments that need a
-        // heuristic re-selection, so spread them over as many waves as possible
-        const size_t rgrid = (size_t)env_double("VSG_REVERSE_GRID", (double)h->reverse_grid);
-        const size_t ppw = std::max<size_t>(1, (size_t)env_double("VSG_REVERSE_PAIRS_PER_WAVE", 16));
-        const int grid = (int)std::max<size_t>(1, std::min<size_t>(rgrid, (npairs + ppw - 1) / ppw));
+        const int grid = (int)std::max<size_t>(1, std::min<size_t>(rgrid, (B.npairs + ppw - 1) / ppw));
         HIP_TRY(launch_reverse(h->st, h->mk, rp, grid, st));
-        HIP_TRY(hipEventRecord(e3, st));
-
-        if (new_top >= 0) {
-            h->entry = order[i + b - 1];
-            h->max_level = new_top;
+        HIP_TRY(hipEventRecord(ev[3], st));
+        if (B.new_top >= 0) {
+            h->entry = order[B.i + B.b - 1];
+            h->max_level = B.new_top;
+        } else {
+            h->entry = B.entry;
+            h->max_level = B.max_level;
         }
         h->build_batches++;
-        i += b;
     }
     h->build_vectors += n;
-    if (nev) {
+    if (!plan.empty()) {
         HIP_TRY(hipStreamSynchronize(st));
-        for (size_t b = 0; b + 3 < nev; b += 4) {
+        for (size_t bi = 0; bi < plan.size(); ++bi) {
             float t[3] = {0.f, 0.f, 0.f};
-            for (int j = 0; j < 3; ++j) HIP_TRY(hipEventElapsedTime(&t[j], h->ev_pool[b + j], h->ev_pool[b + j + 1]));
+            for (int j = 0; j < 3; ++j)
+                HIP_TRY(hipEventElapsedTime(&t[j], h->ev_pool[4 * bi + j], h->ev_pool[4 * bi + j + 1]));
             h->t_insert_ns += (uint64_t)(t[0] * 1e6);
             h->t_sort_ns += (uint64_t)(t[1] * 1e6);
             h->t_reverse_ns += (uint64_t)(t[2] * 1e6);

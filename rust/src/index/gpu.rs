@@ -1,0 +1,263 @@
+//! gpu.rs -- the vector index actor of the reference, on libvsg.so (MI355X, HIP).
+//!
+//! Replaces /root/reference/src/index/usearch.rs:36-311 (`UsearchIndexFactory`, `new`,
+//! `process`, `add_or_replace`, `remove`, `ann`, `count`) behind the unchanged plugin
+//! boundary: `IndexFactory::create_index` returns an `mpsc::Sender<Index>` and the
+//! `Index::{AddOrReplace, Remove, Ann, Count}` messages mean what they meant there.
+//!
+//! What moved into native code: the usearch HNSW (GPU batched build + search kernels)
+//! and the per-message work queue, now `vsg_actor_*` (csrc/actor.hpp), which coalesces
+//! concurrent single-vector adds and single-query anns into batched GPU calls and keeps
+//! the reserve policy of usearch.rs:200-212 (RESERVE_INCREMENT / RESERVE_THRESHOLD).
+//! What stays here, as in the reference: the PrimaryKey <-> u64 BiMap (usearch.rs:109-113),
+//! the dimension checks of `ann` (:259-272) and the key -> PrimaryKey mapping of its result
+//! (:285-301).  Key allocation is monotonic: a replace reuses the live key, a new primary
+//! key takes the next one, nothing is rolled back (the reference's `fetch_sub`
+//! rollback at :191 can hand one key to two primary keys).
+//!
+//! Symbol sequence a lifecycle drives (mirrored by tests/cpp/test_rust_call_sequence.cpp):
+//!   vsg_actor_new (vsg_index_new + reserve(1M)) -> vsg_actor_add_or_replace* ->
+//!   vsg_actor_remove -> vsg_actor_ann -> vsg_actor_count -> vsg_actor_free.
+
+use crate::Connectivity;
+use crate::Dimensions;
+use crate::Embedding;
+use crate::ExpansionAdd;
+use crate::ExpansionSearch;
+use crate::IndexFactory;
+use crate::IndexId;
+use crate::Limit;
+use crate::PrimaryKey;
+use crate::index::actor::AnnR;
+use crate::index::actor::CountR;
+use crate::index::actor::Index;
+use crate::index::vsg_sys as sys;
+use anyhow::anyhow;
+use bimap::BiMap;
+use std::ffi::CStr;
+use std::os::raw::c_int;
+use std::sync::Arc;
+use std::sync::RwLock;
+use tokio::sync::mpsc;
+use tokio::sync::oneshot;
+use tracing::Instrument;
+use tracing::debug;
+use tracing::debug_span;
+use tracing::trace;
+
+/// Status + thread-local message -> anyhow (include/vsg.h "Errors").
+fn check(rc: c_int) -> anyhow::Result<()> {
+    if rc == sys::VSG_OK {
+        return Ok(());
+    }
+    let msg = unsafe { CStr::from_ptr(sys::vsg_last_error()) }.to_string_lossy().into_owned();
+    Err(anyhow!("vsg error {rc}: {msg}"))
+}
+
+/// Owned native actor.  Every vsg_actor_* entry point is thread-safe (vsg.h).
+struct GpuActor(*mut sys::vsg_actor_t);
+unsafe impl Send for GpuActor {}
+unsafe impl Sync for GpuActor {}
+
+impl Drop for GpuActor {
+    fn drop(&mut self) {
+        // drains queued messages, joins the worker, frees the HBM index
+        unsafe { sys::vsg_actor_free(self.0) }
+    }
+}
+
+impl GpuActor {
+    fn new(options: &sys::vsg_actor_options_t) -> anyhow::Result<Self> {
+        let mut a = std::ptr::null_mut();
+        check(unsafe { sys::vsg_actor_new(options, &mut a) })?;
+        Ok(Self(a))
+    }
+
+    fn add_or_replace(&self, key: u64, embedding: &[f32]) -> anyhow::Result<()> {
+        check(unsafe { sys::vsg_actor_add_or_replace(self.0, key, embedding.as_ptr(), embedding.len()) })
+    }
+
+    fn remove(&self, key: u64) -> anyhow::Result<()> {
+        check(unsafe { sys::vsg_actor_remove(self.0, key) })
+    }
+
+    /// Blocks until the batched search holding this query returns.
+    fn ann(&self, embedding: &[f32], limit: usize) -> anyhow::Result<(Vec<u64>, Vec<f32>)> {
+        let mut keys = vec![sys::VSG_NO_KEY; limit];
+        let mut distances = vec![f32::INFINITY; limit];
+        let mut n = 0usize;
+        check(unsafe {
+            sys::vsg_actor_ann(self.0, embedding.as_ptr(), embedding.len(), limit, keys.as_mut_ptr(),
+                               distances.as_mut_ptr(), &mut n)
+        })?;
+        keys.truncate(n);
+        distances.truncate(n);
+        Ok((keys, distances))
+    }
+
+    fn count(&self) -> anyhow::Result<usize> {
+        let mut n = 0usize;
+        check(unsafe { sys::vsg_actor_count(self.0, &mut n) })?;
+        Ok(n)
+    }
+}
+
+/// `IndexFactory` for GPU-backed vector indexes (replaces `UsearchIndexFactory`,
+/// usearch.rs:36-58).  One factory per GPU: every index it creates lives in that
+/// GPU's HBM (row-range sharding over the node's GPUs is the Python/RCCL layer's job,
+/// vsg/distributed.py).
+pub struct GpuIndexFactory {
+    device: i32,
+    metric: u32,
+}
+
+impl IndexFactory for GpuIndexFactory {
+    fn create_index(
+        &self,
+        id: IndexId,
+        dimensions: Dimensions,
+        connectivity: Connectivity,
+        expansion_add: ExpansionAdd,
+        expansion_search: ExpansionSearch,
+    ) -> anyhow::Result<mpsc::Sender<Index>> {
+        new(id, dimensions, connectivity, expansion_add, expansion_search, self.device, self.metric)
+    }
+}
+
+/// GPU `device`, cosine metric.  usearch left the metric to its crate default
+/// (usearch.rs:89-96); here it is explicit.
+pub fn new_gpu(device: i32) -> anyhow::Result<GpuIndexFactory> {
+    Ok(GpuIndexFactory { device, metric: sys::VSG_METRIC_COS })
+}
+
+pub fn new_gpu_with_metric(device: i32, metric: u32) -> anyhow::Result<GpuIndexFactory> {
+    if metric > sys::VSG_METRIC_COS {
+        return Err(anyhow!("unknown metric {metric}"));
+    }
+    Ok(GpuIndexFactory { device, metric })
+}
+
+const CHANNEL_SIZE: usize = 10; // as usearch.rs:102
+
+type Keys = Arc<RwLock<KeyMap>>;
+
+/// PrimaryKey <-> u64 key of the GPU index, with the next free key.
+struct KeyMap {
+    map: BiMap<PrimaryKey, u64>,
+    next: u64,
+}
+
+pub(crate) fn new(
+    id: IndexId,
+    dimensions: Dimensions,
+    connectivity: Connectivity,
+    expansion_add: ExpansionAdd,
+    expansion_search: ExpansionSearch,
+    device: i32,
+    metric: u32,
+) -> anyhow::Result<mpsc::Sender<Index>> {
+    let options = sys::vsg_actor_options_t {
+        index: sys::vsg_index_options_t {
+            dimensions: dimensions.0.get() as u32,
+            metric,
+            quantization: sys::VSG_SCALAR_F32, // ScalarKind::F32, usearch.rs:94
+            connectivity: connectivity.0 as u32, // 0 => usearch defaults (src/db.rs:400-410)
+            expansion_add: expansion_add.0 as u32,
+            expansion_search: expansion_search.0 as u32,
+            device,
+            flags: 0,
+            seed: 0,
+        },
+        // reserve(RESERVE_INCREMENT) up front and the growth rule of usearch.rs:200-212
+        reserve_increment: 1_000_000,
+        reserve_threshold: 1_000_000 / 3,
+        // anns beside writes, as the reference's fire-and-forget adds allow
+        concurrent_reads: 1,
+        ..Default::default()
+    };
+    let actor = Arc::new(GpuActor::new(&options)?);
+    let (tx, mut rx) = mpsc::channel(CHANNEL_SIZE);
+    tokio::spawn(
+        async move {
+            debug!("starting");
+            let keys: Keys = Arc::new(RwLock::new(KeyMap { map: BiMap::new(), next: 0 }));
+            while let Some(msg) = rx.recv().await {
+                process(msg, dimensions, Arc::clone(&actor), Arc::clone(&keys)).await;
+            }
+            debug!("finished");
+        }
+        .instrument(debug_span!("gpu", "{id}")),
+    );
+    Ok(tx)
+}
+
+async fn process(msg: Index, dimensions: Dimensions, actor: Arc<GpuActor>, keys: Keys) {
+    match msg {
+        Index::AddOrReplace { primary_key, embedding } => add_or_replace(&actor, &keys, primary_key, embedding),
+        Index::Remove { primary_key } => remove(&actor, &keys, primary_key),
+        // the native call blocks until its batch is answered: off the async runtime
+        Index::Ann { embedding, limit, tx } => {
+            tokio::task::spawn_blocking(move || ann(&actor, &keys, tx, embedding, dimensions, limit));
+        }
+        Index::Count { tx } => count(&actor, tx),
+    }
+}
+
+/// usearch.rs:174-233.  The native actor removes the live row of a replaced key before
+/// adding (:214-221) and grows capacity; failures are counted there and logged here,
+/// as the reference logs and swallows them (:207-224).
+fn add_or_replace(actor: &GpuActor, keys: &Keys, primary_key: PrimaryKey, embedding: Embedding) {
+    let key = {
+        let mut k = keys.write().unwrap();
+        match k.map.get_by_left(&primary_key) {
+            Some(key) => *key,
+            None => {
+                let key = k.next;
+                k.next += 1;
+                k.map.insert(primary_key, key);
+                key
+            }
+        }
+    };
+    if let Err(err) = actor.add_or_replace(key, &embedding.0) {
+        debug!("add_or_replace: unable to add embedding for key {key}: {err}");
+    }
+}
+
+/// usearch.rs:235-249
+fn remove(actor: &GpuActor, keys: &Keys, primary_key: PrimaryKey) {
+    let Some((_, key)) = keys.write().unwrap().map.remove_by_left(&primary_key) else {
+        return;
+    };
+    if let Err(err) = actor.remove(key) {
+        debug!("remove: unable to remove embedding for key {key}: {err}");
+    }
+}
+
+/// usearch.rs:251-306: dimension checks, search, keys -> primary keys, distances.
+fn ann(actor: &GpuActor, keys: &Keys, tx: oneshot::Sender<AnnR>, embedding: Embedding, dimensions: Dimensions,
+       limit: Limit) {
+    let result = (|| {
+        let len = embedding.0.len();
+        if len == 0 {
+            return Err(anyhow!("ann: embedding dimensions == 0"));
+        }
+        if len != dimensions.0.get() {
+            return Err(anyhow!("ann: wrong embedding dimensions: {len} != {dimensions}"));
+        }
+        let (found, distances) =
+            actor.ann(&embedding.0, limit.0.get()).map_err(|err| anyhow!("ann: search failed: {err}"))?;
+        let k = keys.read().unwrap();
+        let primary_keys = found
+            .into_iter()
+            .map(|key| k.map.get_by_right(&key).cloned().ok_or(anyhow!("not defined primary key column {key}")))
+            .collect::<anyhow::Result<_>>()?;
+        Ok((primary_keys, distances.into_iter().map(|d| d.into()).collect()))
+    })();
+    tx.send(result).unwrap_or_else(|_| trace!("ann: unable to send response"));
+}
+
+/// usearch.rs:308-311 (live size)
+fn count(actor: &GpuActor, tx: oneshot::Sender<CountR>) {
+    tx.send(actor.count()).unwrap_or_else(|_| trace!("count: unable to send response"));
+}

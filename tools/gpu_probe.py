@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""One parameterised GPU probe (replaces round 1's ~45 one-off gpu_*.sh scripts).
+
+  search  build one index (optionally shard s of S row shards), then for every ef and
+          every knob setting (--set KEY=V,KEY=V; VSG_* env knobs) time the device
+          search of the query batch with HIP events on the launching stream and
+          report kernel ms, QPS, distance evaluations / query, algorithmic GB/s
+          (n_dist x row bytes + n_adj x M0 x 4 per launch, no cache credit), fraction
+          of the 8 TB/s HBM roofline, recall@10 against exact ground truth, and
+          whether keys/distances equal the first setting's (same traversal).
+  build   build the index under every knob setting; report build seconds, batches,
+          device time per build kernel and recall at --efs.
+
+Runs unchanged under rocprofv3 (one program, no launcher hops), e.g.
+  rocprofv3 --kernel-trace --stats -d gpurun_out/p -- python3 tools/gpu_probe.py search ...
+  rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/f -- python3 tools/gpu_probe.py search ...
+
+C4 per-shard example (one of 8 row shards of 100M x 128 f16 sift-like):
+  python3 tools/gpu_probe.py search --rows 100000000 --shards 8 --shard 0 --dim 128 \
+      --quant f16 --metric l2sq --data sift --config 3 --efs 64,128,192
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "vector-store-text_amd"))
+
+KNOBS = {"frac": "VSG_BUILD_BATCH_FRAC", "max": "VSG_BUILD_BATCH_MAX", "frac2": "VSG_BUILD_BATCH_FRAC2",
+         "switch": "VSG_BUILD_BATCH_SWITCH", "reg": "VSG_SEARCH_REG", "waves": "VSG_SEARCH_WAVES",
+         "hash": "VSG_SEARCH_HASH_FACTOR", "xcd": "VSG_SEARCH_XCD_MAP", "upper": "VSG_SEARCH_UPPER_EF"}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=("search", "build"))
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--shards", type=int, default=1)
+    ap.add_argument("--shard", type=int, default=0)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--metric", default="cos")
+    ap.add_argument("--quant", default="f32")
+    ap.add_argument("--data", default="clustered")
+    ap.add_argument("--config", type=int, default=1)
+    ap.add_argument("--M", type=int, default=16)
+    ap.add_argument("--efc", type=int, default=128)
+    ap.add_argument("--queries", type=int, default=10_000)
+    ap.add_argument("--gt-queries", type=int, default=1000)
+    ap.add_argument("--efs", default="36,128")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--set", action="append", default=[])
+    return ap.parse_args()
+
+
+def apply(setting):
+    env = dict(kv.split("=") for kv in setting.split(",") if kv)
+    for k, v in env.items():
+        os.environ[KNOBS.get(k, k)] = v
+    return env
+
+
+def clear(env):
+    for k in env:
+        os.environ.pop(KNOBS.get(k, k), None)
+
+
+def build(a, x):
+    import torch
+    import vsg
+    lo = a.shard * a.rows // a.shards
+    idx = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 64, seed=0x5EED + a.shard)
+    idx.reserve(x.shape[0])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    idx.add_device(np.arange(lo, lo + x.shape[0], dtype=np.uint64), x)
+    torch.cuda.synchronize()
+    return idx, time.perf_counter() - t0
+
+
+def recall(f, gt, k):
+    return round(float(np.mean([len(set(f[i]) & set(gt[i])) / k for i in range(gt.shape[0])])), 4)
+
+
+def main():
+    a = parse()
+    import torch
+
+    import vsg
+    from vsg import datagen as G
+    bs, qs, ms = G.config_seeds(a.config)
+    lo, hi = a.shard * a.rows // a.shards, (a.shard + 1) * a.rows // a.shards
+    x = vsg.datagen_device(a.data, hi - lo, a.dim, bs, ms, start=lo)
+    q = vsg.datagen_device(a.data, a.queries, a.dim, qs, ms)
+    qg = q[: a.gt_queries].contiguous()
+    per16 = 4 if a.quant == "f32" else 8
+    row_bytes = (a.dim + per16 - 1) // per16 * 16
+    efs = [int(e) for e in a.efs.split(",")]
+    stream = torch.cuda.current_stream()
+    head = {"rows": hi - lo, "of_rows": a.rows, "dim": a.dim, "metric": a.metric, "quant": a.quant,
+            "data": a.data, "queries": a.queries}
+    if a.mode == "build":
+        gt = None
+        for st in a.set or [""]:
+            env = apply(st)
+            idx, bt = build(a, x)
+            if gt is None:
+                gt = idx.search_device(qg, a.k, exact=True)[0].cpu().numpy()
+            s = idx.stats()
+            out = dict(head, set=st, build_s=round(bt, 3), build_vps=round((hi - lo) / bt, 1),
+                       batches=s["build_batches"],
+                       kernel_s={k: round(s[f"build_{k}_ns"] * 1e-9, 4) for k in ("insert", "sort", "reverse")})
+            for ef in efs:
+                out[f"recall_ef{ef}"] = recall(idx.search_device(qg, a.k, ef)[0].cpu().numpy(), gt, a.k)
+            print(json.dumps(out), flush=True)
+            clear(env)
+            del idx
+        return
+    idx, bt = build(a, x)
+    del x
+    gt = idx.search_device(qg, a.k, exact=True)[0].cpu().numpy()
+    print(json.dumps(dict(head, build_s=round(bt, 3))), flush=True)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for ef in efs:
+        base = None
+        for st in a.set or [""]:
+            env = apply(st)
+            kk, dd = idx.search_device(q, a.k, ef, stream=stream)
+            torch.cuda.synchronize()
+            kk, dd = kk.cpu().numpy(), dd.cpu().numpy()
+            if base is None:
+                base = (kk, dd)
+            same = bool((kk == base[0]).all() and (dd == base[1]).all())
+            idx.reset_stats()
+            ms_k = 0.0
+            for _ in range(a.steps):
+                ev0.record(stream)
+                idx.search_device(q, a.k, ef, stream=stream)
+                ev1.record(stream)
+                torch.cuda.synchronize()
+                ms_k += ev0.elapsed_time(ev1)
+            ms_k /= a.steps
+            s = idx.stats()
+            nq = max(1, s["search_queries"])
+            alg = (s["search_distances"] * row_bytes + s["search_adjacency"] * 2 * a.M * 4) / a.steps
+            gbs = alg / (ms_k * 1e-3) / 1e9
+            print(json.dumps(dict(head, ef=ef, set=st, kernel_ms=round(ms_k, 3), qps=round(a.queries / ms_k * 1e3, 1),
+                                  dist_per_query=round(s["search_distances"] / nq, 1),
+                                  adj_per_query=round(s["search_adjacency"] / nq, 1),
+                                  alg_bytes_per_launch=int(alg), achieved_gbs=round(gbs, 1),
+                                  hbm_frac=round(gbs / 8000.0, 4),
+                                  recall_at_10=recall(kk[: a.gt_queries], gt, a.k), same_as_first=same)),
+                  flush=True)
+            clear(env)
+
+
+if __name__ == "__main__":
+    main()

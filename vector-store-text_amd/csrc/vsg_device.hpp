@@ -135,9 +135,27 @@ template <int G, int VM, typename T> struct QReg {
     }
 };
 
+// 16-B chunk -> E floats (f16 converted exactly to f32)
+template <typename T>
+__device__ __forceinline__ void unpack_chunk(const uint4 raw, float (&out)[ChunkT<T>::E]) {
+    if constexpr (sizeof(T) == 4) {
+        out[0] = __uint_as_float(raw.x);
+        out[1] = __uint_as_float(raw.y);
+        out[2] = __uint_as_float(raw.z);
+        out[3] = __uint_as_float(raw.w);
+    } else {
+        half8_t h = __builtin_bit_cast(half8_t, raw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) out[e] = (float)h[e];
+    }
+}
+
 // Distances from the register image q to `count` rows listed in ids[] (LDS),
-// written to out[] (LDS).  Wave-uniform count.  Returns nothing; out[r] holds
-// the metric distance (l2sq, or 1 - dot).
+// written to out[] (LDS).  Wave-uniform count.  out[r] holds the metric
+// distance (l2sq, or 1 - dot).  All U x VM chunk loads of a pass are issued
+// before any arithmetic and kept as raw 16-B words (4 VGPRs each; f16 rows are
+// widened to f32 only when consumed), so the loads in flight cost half the
+// registers for f16 rows.
 template <int G, int VM, int U, typename T, int MET>
 __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size_t row_bytes,
                                           int nchunks, const uint32_t* ids, int count,
@@ -148,7 +166,7 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
     const int sub = lane / G;
     const int sl = lane % G;
     for (int base = 0; base < count; base += R * U) {
-        float buf[U][VM][E];
+        uint4 raw[U][VM];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int r = base + u * R + sub;
@@ -157,7 +175,7 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
 #pragma unroll
             for (int v = 0; v < VM; ++v) {
                 const int c = v * G + sl;
-                load_chunk<T>(row, c < nchunks ? c : nchunks - 1, buf[u][v]);
+                raw[u][v] = *reinterpret_cast<const uint4*>(row + (size_t)(c < nchunks ? c : nchunks - 1) * 16);
             }
         }
 #pragma unroll
@@ -166,14 +184,16 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
 #pragma unroll
             for (int v = 0; v < VM; ++v) {
                 const bool live = (v * G + sl) < nchunks;
+                float x[E];
+                unpack_chunk<T>(raw[u][v], x);
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
                     float t;
                     if constexpr (MET == MET_L2) {
-                        const float df = buf[u][v][e] - q.x[v][e];
+                        const float df = x[e] - q.x[v][e];
                         t = df * df;
                     } else {
-                        t = buf[u][v][e] * q.x[v][e];
+                        t = x[e] * q.x[v][e];
                     }
                     acc += live ? t : 0.f;
                 }
@@ -199,7 +219,7 @@ __device__ __forceinline__ void rows_dist2(const uint8_t* __restrict__ vecs, siz
     const int sub = lane / G;
     const int sl = lane % G;
     for (int base = 0; base < count; base += R * U) {
-        float buf[U][VM][E];
+        uint4 raw[U][VM];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int r = base + u * R + sub;
@@ -208,7 +228,7 @@ __device__ __forceinline__ void rows_dist2(const uint8_t* __restrict__ vecs, siz
 #pragma unroll
             for (int v = 0; v < VM; ++v) {
                 const int c = v * G + sl;
-                load_chunk<T>(row, c < nchunks ? c : nchunks - 1, buf[u][v]);
+                raw[u][v] = *reinterpret_cast<const uint4*>(row + (size_t)(c < nchunks ? c : nchunks - 1) * 16);
             }
         }
 #pragma unroll
@@ -217,17 +237,19 @@ __device__ __forceinline__ void rows_dist2(const uint8_t* __restrict__ vecs, siz
 #pragma unroll
             for (int v = 0; v < VM; ++v) {
                 const bool live = (v * G + sl) < nchunks;
+                float x[E];
+                unpack_chunk<T>(raw[u][v], x);
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
                     float t0, t1;
                     if constexpr (MET == MET_L2) {
-                        const float d0 = buf[u][v][e] - q0.x[v][e];
-                        const float d1 = buf[u][v][e] - q1.x[v][e];
+                        const float d0 = x[e] - q0.x[v][e];
+                        const float d1 = x[e] - q1.x[v][e];
                         t0 = d0 * d0;
                         t1 = d1 * d1;
                     } else {
-                        t0 = buf[u][v][e] * q0.x[v][e];
-                        t1 = buf[u][v][e] * q1.x[v][e];
+                        t0 = x[e] * q0.x[v][e];
+                        t1 = x[e] * q1.x[v][e];
                     }
                     a0 += live ? t0 : 0.f;
                     a1 += live ? t1 : 0.f;

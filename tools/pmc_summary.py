@@ -1,15 +1,17 @@
-"""HBM traffic of the search kernel from rocprofv3 PMC passes.
+"""HBM traffic from rocprofv3 PMC passes (one counter per pass, MI355X_MICROARCH.md).
 
-usage: python tools/pmc_summary.py <fetch_dir> <write_dir> n dim queries ef metric
-Each dir is the output of its own pass:
+  search: python tools/pmc_summary.py search <fetch_dir> <write_dir> n dim queries ef metric [out.json]
+          -> profiles/search_pmc.json: bytes per search launch (the bench workload's grid)
+  build:  python tools/pmc_summary.py build <fetch_dir> <write_dir> n dim metric M efc [out.json]
+          -> profiles/build_pmc.json: bytes over ALL insert / reverse launches of one build
+
+Each dir is the output of its own pass, e.g.
   rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d <dir> -- python3 bench.py ...
   rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d <dir> -- python3 bench.py ...
-FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction
-(MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of 16-B/lane
-coalesced streaming reads -> x2 (the search kernel's row loads are 16 B/lane,
-1 KiB contiguous per wave instruction; the 4-B adjacency loads are a small
-share and are doubled too, which over-states them).  WRITE_SIZE is taken as-is.
-Writes profiles/search_pmc.json, read by bench.py for roofline.traffic.
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  gfx950 correction (MI355X_MICROARCH.md
+§HBM): FETCH_SIZE reports half the bytes of 16-B/lane coalesced streaming reads -> x2 (the
+row loads are 16 B/lane; the 4-B adjacency loads are a small share and are doubled too,
+which over-states them).  WRITE_SIZE is taken as-is.
 """
 import csv
 import glob
@@ -18,27 +20,29 @@ import os
 import sys
 from collections import defaultdict
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-def per_dispatch(d, counter):
+
+def per_dispatch(d, counter, kernel):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
     vals = defaultdict(float)
     grid = {}
-    for r in csv.DictReader(open(files[0])):
-        if r.get("Counter_Name") != counter or "hnsw_search_" not in r.get("Kernel_Name", ""):
-            continue
-        key = r.get("Dispatch_Id") or r.get("Correlation_Id")
-        vals[key] += float(r["Counter_Value"])
-        grid[key] = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter or kernel not in r.get("Kernel_Name", ""):
+                continue
+            key = (f, r.get("Dispatch_Id") or r.get("Correlation_Id"))
+            vals[key] += float(r["Counter_Value"])
+            grid[key] = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
     return vals, grid
 
 
-def main():
-    fdir, wdir, n, dim, nq, ef, metric = sys.argv[1:8]
+def search(fdir, wdir, n, dim, nq, ef, metric, path=None):
     nq = int(nq)
-    fv, fg = per_dispatch(fdir, "FETCH_SIZE")
-    wv, wg = per_dispatch(wdir, "WRITE_SIZE")
+    fv, fg = per_dispatch(fdir, "FETCH_SIZE", "hnsw_search_")
+    wv, wg = per_dispatch(wdir, "WRITE_SIZE", "hnsw_search_")
     full = [k for k in fv if fg[k] == nq * 64]
     fullw = [k for k in wv if wg[k] == nq * 64]
     if not full:
@@ -54,10 +58,25 @@ def main():
         "hbm_bytes_per_launch": int(2 * fetch_kib * 1024 + write_kib * 1024),
         "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes",
     }
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    json.dump(out, open(os.path.join(root, "profiles", "search_pmc.json"), "w"), indent=1)
-    print(json.dumps(out))
+    json.dump(out, open(path or os.path.join(ROOT, "profiles", "search_pmc.json"), "w"), indent=1)
+    return out
+
+
+def build(fdir, wdir, n, dim, metric, M, efc, path=None):
+    out = {"workload": {"n": int(n), "dim": int(dim), "metric": metric, "M": int(M), "efc": int(efc)},
+           "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes; summed over every "
+                         "dispatch of the kernel in ONE build (the probe builds once per process)"}
+    for tag, kern in (("insert", "hnsw_insert_kernel"), ("reverse", "hnsw_reverse_kernel")):
+        fv, _ = per_dispatch(fdir, "FETCH_SIZE", kern)
+        wv, _ = per_dispatch(wdir, "WRITE_SIZE", kern)
+        out[f"{tag}_dispatches"] = len(fv)
+        out[f"{tag}_fetch_kib_raw"] = round(sum(fv.values()), 1)
+        out[f"{tag}_write_kib_raw"] = round(sum(wv.values()), 1)
+        out[f"{tag}_hbm_bytes"] = int(2 * sum(fv.values()) * 1024 + sum(wv.values()) * 1024)
+    json.dump(out, open(path or os.path.join(ROOT, "profiles", "build_pmc.json"), "w"), indent=1)
+    return out
 
 
 if __name__ == "__main__":
-    main()
+    mode = sys.argv[1]
+    print(json.dumps(search(*sys.argv[2:10]) if mode == "search" else build(*sys.argv[2:10])))

@@ -204,6 +204,8 @@ __device__ __forceinline__ void admit(RegSet<R>& B, bool mine, uint64_t ck, bool
 // alongside (its adjacency row and distances in the same round trips,
 // committed only when it is the sequential next step) was measured 0-15%
 // slower: the runner-up is rarely still next (profiles/r01_search_phases.jsonl).
+// Prefetching only the runner-up's adjacency row: C4 shard search -8 %, C2
+// search +2 %, C2 build -5 % (profiles/r02_search_probes.jsonl) -- not kept.
 template <int G, int VM, int U, typename T, int MET, int R>
 __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t ep, float dep, int ef, WaveLds& w,
                          RegSet<R>& B, uint64_t& ndist, uint64_t& nadj, BeamProf& pf) {
@@ -245,6 +247,9 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
     bool lossy = false;
     uint64_t* sk = reinterpret_cast<uint64_t*>(w.sd);  // sd + si: 64 x 8 B
     wave_sync();
+    auto row_of = [&](uint32_t n) {
+        return l == 0 ? adj0 + (size_t)n * m0r : upper + ((size_t)upper_off[n] + (size_t)(l - 1)) * mr;
+    };
     for (;;) {
         const uint64_t t0 = VSG_CLK();
         const uint64_t a = B.min_unexpanded();
@@ -252,7 +257,7 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
         if (B.size > ef && B.count_below(a) >= ef) break;
         B.mark_expanded(a);
         const uint32_t na = (uint32_t)a & VSG_ID_MASK;
-        const uint32_t* row = l == 0 ? adj0 + (size_t)na * m0r : upper + ((size_t)upper_off[na] + (size_t)(l - 1)) * mr;
+        const uint32_t* row = row_of(na);
         ++nadj;
         // one 64-entry piece of the row per pass (M0 = 2M <= 128); the expansion's
         // pieces are admitted one after another, which leaves the same set as one

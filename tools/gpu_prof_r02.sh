@@ -12,5 +12,5 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format cs
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 -- $P $C4 > gpurun_out/prof_c4.log 2>&1 || exit 1
 python3 tools/pmc_summary.py build gpurun_out/pmc_bf gpurun_out/pmc_bw 1000000 768 cos 16 128 gpurun_out/build_pmc.json
 python3 tools/pmc_summary.py search gpurun_out/pmc_c4f gpurun_out/pmc_c4w 12500000 128 100000 192 l2sq gpurun_out/c4_search_pmc.json
-python3 tools/prof_summary.py gpurun_out/prof_c4 > gpurun_out/prof_c4_summary.md || true
+find gpurun_out/prof_c4 -name '*kernel_trace.csv' -delete  # keep the small stats CSV
 rm -rf gpurun_out/pmc_bf gpurun_out/pmc_bw gpurun_out/pmc_c4f gpurun_out/pmc_c4w  # > 64 MiB of CSV

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/vsg.h"
@@ -87,6 +88,21 @@ int sample_level(uint64_t seed, uint64_t slot, uint32_t connectivity) {
     double lv = -log(u) / log((double)connectivity);
     int l = (int)lv;
     return l > 30 ? 30 : l;
+}
+
+// f(lo, hi) over [0, n) on up to 16 host threads (bulk adds: level draws of
+// 10^7+ slots would otherwise hold the index lock for a large part of a second)
+template <typename F>
+void host_parallel(size_t n, F&& f) {
+    const size_t T = std::min<size_t>(16, std::max<unsigned>(1, std::thread::hardware_concurrency()));
+    if (n < ((size_t)1 << 16) || T == 1) {
+        f((size_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t step = (n + T - 1) / T;
+    for (size_t lo = 0; lo < n; lo += step) th.emplace_back([&f, lo, n, step] { f(lo, std::min(n, lo + step)); });
+    for (auto& t : th) t.join();
 }
 
 double env_double(const char* name, double dflt) {
@@ -376,9 +392,14 @@ static int stage_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* keys
     // levels and upper rows
     std::vector<uint32_t> upper_off(n);
     size_t need_upper = h->upper_used;
+    int8_t* lv = h->h_levels.data() + s0;
+    const uint32_t M = (uint32_t)h->M;
+    const uint64_t seed = h->opt.seed;
+    host_parallel(n, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) lv[i] = (int8_t)sample_level(seed, s0 + i, M);
+    });
     for (size_t i = 0; i < n; ++i) {
-        const int L = sample_level(h->opt.seed, s0 + i, (uint32_t)h->M);
-        h->h_levels[s0 + i] = (int8_t)L;
+        const int L = lv[i];
         upper_off[i] = L > 0 ? (uint32_t)need_upper : 0xFFFFFFFFu;
         need_upper += (size_t)L;
     }
@@ -431,11 +452,15 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         int max_level;
         int new_top;  // > max_level: the batch's last node becomes the entry
     };
-    const double frac = env_double("VSG_BUILD_BATCH_FRAC", 1.0 / 16.0);
+    // batch = frac x graph size, at most bmax (and at least 8 batches per call).
+    // Round 2 sweep at C2 (profiles/r02_build_schedule.jsonl, recall@10 on 10k
+    // queries): 1/16 & 32k 1.00 s, recall 0.957; 1/2 & 64k 0.77 s, 0.959 -- the
+    // early, latency-bound batches were the cost, and larger ones lose no recall.
+    const double frac = env_double("VSG_BUILD_BATCH_FRAC", 0.5);
     // probe knobs: a second batch fraction once the graph holds `switch_at` nodes
     const double frac2 = env_double("VSG_BUILD_BATCH_FRAC2", frac);
     const double switch_at = env_double("VSG_BUILD_BATCH_SWITCH", 0);
-    const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 32768);
+    const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 65536);
     // at least 8 batches per call, so the call's own nodes find each other
     const size_t bcall = std::max<size_t>(1, n / 8);
     std::vector<uint32_t> pair_off(n);

@@ -113,7 +113,10 @@ def main():
             s = idx.stats()
             out = dict(head, set=st, build_s=round(bt, 3), build_vps=round((hi - lo) / bt, 1),
                        batches=s["build_batches"],
-                       kernel_s={k: round(s[f"build_{k}_ns"] * 1e-9, 4) for k in ("insert", "sort", "reverse")})
+                       kernel_s={k: round(s[f"build_{k}_ns"] * 1e-9, 4) for k in ("insert", "sort", "reverse")},
+                       per_vector={k: round(s[k] / max(1, hi - lo), 2) for k in (
+                           "build_distances", "build_select_distances", "reverse_recompute_distances",
+                           "reverse_select_distances", "build_adjacency", "reverse_prunes", "reverse_appends")})
             for ef in efs:
                 out[f"recall_ef{ef}"] = recall(idx.search_device(qg, a.k, ef)[0].cpu().numpy(), gt, a.k)
             print(json.dumps(out), flush=True)

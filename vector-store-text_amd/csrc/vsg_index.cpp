@@ -530,10 +530,11 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     HIP_TRY(hipMemcpyAsync(h->d_blevels, blev.data(), n, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_pair_off, pair_off.data(), n * 4, hipMemcpyHostToDevice, st));
 
-    // a few pairs per wave: the cost is in the few segments that need a
-    // heuristic re-selection, so spread them over as many waves as possible
+    // pairs per reverse-kernel wave: with batches of up to 64k nodes, 64 pairs a
+    // wave beat 16 (round 1's choice for 1/16-graph batches): C2 reverse 0.120 ->
+    // 0.075 s, C4 shard 1.32 -> 0.74 s (profiles/r02_build_schedule.jsonl)
     const size_t rgrid = (size_t)env_double("VSG_REVERSE_GRID", (double)h->reverse_grid);
-    const size_t ppw = std::max<size_t>(1, (size_t)env_double("VSG_REVERSE_PAIRS_PER_WAVE", 16));
+    const size_t ppw = std::max<size_t>(1, (size_t)env_double("VSG_REVERSE_PAIRS_PER_WAVE", 64));
     const int hash = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", 16));
     for (size_t bi = 0; bi < plan.size(); ++bi) {
         const Batch& B = plan[bi];

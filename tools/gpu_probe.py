@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--set", action="append", default=[])
+    ap.add_argument("--seeds", default="0", help="build mode: index seeds (offsets from the default)")
+    ap.add_argument("--phases", action="store_true",
+                    help="build mode, with VSG_LIB_PATH=lib_prof/libvsg.so (make prof): insert-wave "
+                         "clock split into beam / heuristic selection")
     return ap.parse_args()
 
 
@@ -69,11 +73,11 @@ def clear(env):
         os.environ.pop(KNOBS.get(k, k), None)
 
 
-def build(a, x):
+def build(a, x, seed=0):
     import torch
     import vsg
     lo = a.shard * a.rows // a.shards
-    idx = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 64, seed=0x5EED + a.shard)
+    idx = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 64, seed=0x5EED + a.shard + seed)
     idx.reserve(x.shape[0])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -105,18 +109,26 @@ def main():
             "data": a.data, "queries": a.queries}
     if a.mode == "build":
         gt = None
-        for st in a.set or [""]:
+        for st, seed in [(st, int(sd)) for st in a.set or [""] for sd in a.seeds.split(",")]:
             env = apply(st)
-            idx, bt = build(a, x)
+            idx, bt = build(a, x, seed)
             if gt is None:
                 gt = idx.search_device(qg, a.k, exact=True)[0].cpu().numpy()
             s = idx.stats()
-            out = dict(head, set=st, build_s=round(bt, 3), build_vps=round((hi - lo) / bt, 1),
+            out = dict(head, set=st, seed=seed, build_s=round(bt, 3), build_vps=round((hi - lo) / bt, 1),
                        batches=s["build_batches"],
                        kernel_s={k: round(s[f"build_{k}_ns"] * 1e-9, 4) for k in ("insert", "sort", "reverse")},
                        per_vector={k: round(s[k] / max(1, hi - lo), 2) for k in (
                            "build_distances", "build_select_distances", "reverse_recompute_distances",
                            "reverse_select_distances", "build_adjacency", "reverse_prunes", "reverse_appends")})
+            if a.phases:
+                import ctypes as C
+                from vsg._lib import lib
+                raw = (C.c_uint64 * 16)()
+                lib().vsg_debug_counters(idx._h, raw)
+                tot = max(1, raw[10])
+                out["insert_wave_clock_share"] = {"beam": round(raw[15] / tot, 3), "select": round(raw[14] / tot, 3),
+                                                  "other": round(1 - (raw[14] + raw[15]) / tot, 3)}
             for ef in efs:
                 out[f"recall_ef{ef}"] = recall(idx.search_device(qg, a.k, ef)[0].cpu().numpy(), gt, a.k)
             print(json.dumps(out), flush=True)

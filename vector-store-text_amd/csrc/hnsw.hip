@@ -106,73 +106,66 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
 
 // usearch refine_ restated (oracle select_heuristic()): walk the sorted list,
 // keep c unless a kept r has dist(c, r) < dist(c, base).  Returns #kept.
+// Candidates go in blocks of NQ held in VGPRs: the block is tested against the
+// kept set in one pass over its rows (each row loaded once, rows_test), then
+// each candidate, in list order, against the block's earlier kept candidates
+// from registers -- the sequential decision for every candidate, with the same
+// distance values.  NQ = 2 halves the kept-row loads of one-at-a-time
+// (single: insert kernel +20 % time); NQ = 4 halves them again.
+#ifndef VSG_SEL_BLOCK
+#define VSG_SEL_BLOCK 4
+#endif
+#ifndef VSG_SEL_U
+#define VSG_SEL_U 1
+#endif
 template <int G, int VM, int U, typename T, int MET>
 __device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uint64_t& ndist) {
-    // Candidates go in pairs (c0, c1): both are tested against the kept set in
-    // one pass over its rows (each row loaded once, rows_dist2); c1 is then
-    // also tested against c0 if c0 was kept -- the sequential decision for
-    // both, with the same distance values.  The next pair's rows stream in
-    // under the current tests.
-    constexpr int BLK = (64 / G) * U;
+    constexpr int NQ = VSG_SEL_BLOCK;
+    constexpr int UT = VSG_SEL_U < U ? VSG_SEL_U : U;  // row passes in flight per test
+    constexpr int BLK = (64 / G) * UT;
     const int lane = lane_id();
     List& L = w.list;
     int kept = 0;
     using Q = QReg<G, VM, T>;
-    uint4 raw0[VM], raw1[VM];
-    if (n > 0) Q::fetch(g.vec(L.I()[0] & VSG_ID_MASK), g.nchunks, raw0);
-    if (n > 1) Q::fetch(g.vec(L.I()[1] & VSG_ID_MASK), g.nchunks, raw1);
-    float* d1out = w.sd;  // 64-entry scratch beside tdist
-    for (int i = 0; i < n && kept < m; i += 2) {
-        const bool two = i + 1 < n;
-        const uint32_t c0 = L.I()[i] & VSG_ID_MASK;
-        const float cd0 = L.D()[i];
-        const uint32_t c1 = two ? (L.I()[i + 1] & VSG_ID_MASK) : 0u;
-        const float cd1 = two ? L.D()[i + 1] : 0.f;
-        Q q0, q1;
-        q0.set(raw0, g.nchunks);
-        q1.set(raw1, g.nchunks);
-        if (i + 2 < n) Q::fetch(g.vec(L.I()[i + 2] & VSG_ID_MASK), g.nchunks, raw0);
-        if (i + 3 < n) Q::fetch(g.vec(L.I()[i + 3] & VSG_ID_MASK), g.nchunks, raw1);
-        bool good0 = true, good1 = two;
-        for (int b = 0; b < kept && (good0 || good1); b += BLK) {
+    for (int i = 0; i < n && kept < m; i += NQ) {
+        const int nb = min(NQ, n - i);
+        Q qc[NQ];
+        float cd[NQ];
+        uint32_t cid[NQ];
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            const int jj = j < nb ? i + j : i;  // a short last block repeats its head (masked off)
+            cid[j] = L.I()[jj] & VSG_ID_MASK;
+            cd[j] = L.D()[jj];
+            qc[j].load(g.vec(cid[j]), g.nchunks);
+        }
+        uint32_t alive = (1u << nb) - 1u;
+        for (int b = 0; b < kept && alive; b += BLK) {
             const int cnt = min(BLK, kept - b);
-            if (good1) {
-                rows_dist2<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.sel + b, cnt, q0, q1, w.tdist, d1out);
-                ndist += 2 * (uint64_t)cnt;
-            } else {
-                rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.sel + b, cnt, q0, w.tdist);
-                ndist += (uint64_t)cnt;
+            ndist += (uint64_t)cnt * (uint64_t)__popc(alive);
+            alive &= ~rows_test<NQ, G, VM, UT, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.sel + b, cnt, qc, cd);
+        }
+        uint32_t kb = 0;  // block members kept so far
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            bool good = ((alive >> j) & 1u) && kept < m;
+#pragma unroll
+            for (int t = 0; t < j; ++t) {
+                if (good && ((kb >> t) & 1u)) {
+                    ++ndist;
+                    if (reg_dist<G, VM, T, MET>(qc[j], qc[t], g.nchunks) < cd[j]) good = false;
+                }
             }
-            wave_sync();
-            if (good0 && __ballot(lane < cnt && w.tdist[lane] < cd0)) good0 = false;
-            if (good1 && __ballot(lane < cnt && d1out[lane] < cd1)) good1 = false;
-            wave_sync();
-        }
-        if (good0) {
-            if (lane == 0) {
-                w.sel[kept] = c0;
-                w.seld[kept] = cd0;
+            if (good) {
+                if (lane == 0) {
+                    w.sel[kept] = cid[j];
+                    w.seld[kept] = cd[j];
+                }
+                kb |= 1u << j;
+                ++kept;
             }
-            ++kept;
-            wave_sync();
         }
-        if (!two || kept >= m || !good1) continue;
-        if (good0) {
-            // c1 against the just-kept c0
-            rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.sel + kept - 1, 1, q1, w.tdist);
-            wave_sync();
-            ++ndist;
-            good1 = !(w.tdist[0] < cd1);
-            wave_sync();
-        }
-        if (good1) {
-            if (lane == 0) {
-                w.sel[kept] = c1;
-                w.seld[kept] = cd1;
-            }
-            ++kept;
-            wave_sync();
-        }
+        wave_sync();
     }
     return kept;
 }
@@ -421,6 +414,7 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     const int L = p.levels[bi];
     uint64_t ndist = 0, nadj = 0, nsel_d = 0;
     BeamProf pf;
+    uint64_t tsel = 0;
     QReg<G, VM, T> q;
     q.load(g.vec(node), g.nchunks);
     uint32_t cur = p.entry;
@@ -439,7 +433,9 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
             beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, pf);
         }
         const int m = l == 0 ? g.M0 : g.M;
+        const uint64_t ts = VSG_CLK();
         const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, m, nsel_d);
+        tsel += VSG_CLK() - ts;
         uint32_t* row = g.row(node, l);
         for (int j = lane; j < m; j += 64) row[j] = j < nsel ? w.sel[j] : VSG_EMPTY;
         for (int j = lane; j < nsel; j += 64) {
@@ -461,8 +457,11 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
         atomicAdd(&p.stats[10], dt);
         atomicMax(&p.stats[11], dt);
 #ifdef VSG_SEARCH_PROFILE
-        atomicAdd(&p.stats[14], (unsigned long long)pf.merge);
-        atomicAdd(&p.stats[15], (unsigned long long)(pf.adj + pf.dist));
+        // profile build: [14] heuristic selection, [15] beam (adjacency + rows + merge)
+        atomicAdd(&p.stats[14], (unsigned long long)tsel);
+        atomicAdd(&p.stats[15], (unsigned long long)(pf.adj + pf.dist + pf.merge));
+#else
+        (void)tsel;
 #endif
     }
 }

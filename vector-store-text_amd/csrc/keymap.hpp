@@ -4,8 +4,10 @@
 // erase (rebuilt on growth).  ~10x faster and ~3x smaller than std::unordered_map
 // at 10^8 keys, which is what bulk loads of C4 (100M rows) need.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <vector>
 
 namespace vsg {
@@ -60,6 +62,60 @@ class KeyMap {
                 return true;
             }
         }
+    }
+
+    // Bulk insert keys[i] -> s0 + i (i < n) with pfor(n, f(lo, hi)) workers:
+    // the table is sized first (no resize while they run), then each bucket is
+    // claimed with a CAS on EMPTY -- lock-free linear probing; tombstones are not
+    // reused here.  All or nothing: on a reserved key, a live duplicate or a
+    // duplicate inside the batch every key this call inserted is erased again and
+    // false is returned (the caller re-runs insert() serially for its error).
+    template <class PF>
+    bool insert_all(const uint64_t* keys, size_t n, uint32_t s0, PF&& pfor) {
+        if (n == 0) return true;
+        if ((used_ + n) * 2 > cap_) {
+            size_t want = cap_ ? cap_ : 16;
+            while (want < 2 * (live_ + n) + 2) want <<= 1;
+            rehash(want);
+        }
+        uint64_t* kk = keys_.data();
+        uint32_t* vv = vals_.data();
+        const size_t mask = cap_ - 1;
+        std::atomic<bool> ok{true};
+        std::atomic<size_t> added{0};
+        pfor(n, [&](size_t lo, size_t hi) {
+            size_t mine = 0;
+            for (size_t i = lo; i < hi && ok.load(std::memory_order_relaxed); ++i) {
+                const uint64_t k = keys[i];
+                if (k >= DEAD) {
+                    ok = false;
+                    break;
+                }
+                for (size_t b = hash(k) & mask;; b = (b + 1) & mask) {
+                    uint64_t cur = __atomic_load_n(&kk[b], __ATOMIC_ACQUIRE);
+                    if (cur == EMPTY &&
+                        __atomic_compare_exchange_n(&kk[b], &cur, k, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+                        vv[b] = s0 + (uint32_t)i;
+                        ++mine;
+                        break;
+                    }
+                    if (cur == k) {  // live key, or a duplicate claimed by another worker
+                        ok = false;
+                        break;
+                    }
+                }
+                if (!ok.load(std::memory_order_relaxed)) break;
+            }
+            added += mine;
+        });
+        used_ += added;
+        live_ += added;
+        if (ok) return true;
+        for (size_t i = 0; i < n; ++i) {
+            uint32_t v;
+            if (find(keys[i], &v) && v >= s0 && v - s0 < n) erase(keys[i], nullptr);
+        }
+        return false;
     }
 
     void reserve(size_t n) {

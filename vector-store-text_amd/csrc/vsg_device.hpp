@@ -269,6 +269,100 @@ __device__ __forceinline__ void rows_dist2(const uint8_t* __restrict__ vecs, siz
     }
 }
 
+// The heuristic selection's test for NQ register-held candidates at once: bit j
+// of the result is set if some listed row r has dist(q[j], r) < lim[j].  Each
+// row is loaded once for all NQ candidates; distances are the values rows_dist
+// computes (same per-lane order and shuffle tree), reduced to a ballot instead
+// of an LDS write.  Wave-uniform count.
+template <int NQ, int G, int VM, int U, typename T, int MET>
+__device__ __forceinline__ uint32_t rows_test(const uint8_t* __restrict__ vecs, size_t row_bytes, int nchunks,
+                                              const uint32_t* ids, int count, const QReg<G, VM, T> (&q)[NQ],
+                                              const float (&lim)[NQ]) {
+    constexpr int R = 64 / G;
+    constexpr int E = ChunkT<T>::E;
+    const int lane = lane_id();
+    const int sub = lane / G;
+    const int sl = lane % G;
+    uint32_t hit = 0;
+    for (int base = 0; base < count; base += R * U) {
+        uint4 raw[U][VM];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = base + u * R + sub;
+            const int rr = r < count ? r : count - 1;
+            const uint8_t* row = vecs + (size_t)ids[rr] * row_bytes;
+#pragma unroll
+            for (int v = 0; v < VM; ++v) {
+                const int c = v * G + sl;
+                raw[u][v] = *reinterpret_cast<const uint4*>(row + (size_t)(c < nchunks ? c : nchunks - 1) * 16);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float a[NQ];
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) a[j] = 0.f;
+#pragma unroll
+            for (int v = 0; v < VM; ++v) {
+                const bool live = (v * G + sl) < nchunks;
+                float x[E];
+                unpack_chunk<T>(raw[u][v], x);
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+#pragma unroll
+                    for (int j = 0; j < NQ; ++j) {
+                        float t;
+                        if constexpr (MET == MET_L2) {
+                            const float df = x[e] - q[j].x[v][e];
+                            t = df * df;
+                        } else {
+                            t = x[e] * q[j].x[v][e];
+                        }
+                        a[j] += live ? t : 0.f;
+                    }
+                }
+            }
+            const int r = base + u * R + sub;
+            const bool ok = sl == 0 && r < count;
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+#pragma unroll
+                for (int o = G / 2; o > 0; o >>= 1) a[j] += __shfl_xor(a[j], o);
+                const float d = (MET == MET_L2) ? a[j] : 1.f - a[j];
+                if (__ballot(ok && d < lim[j])) hit |= 1u << j;
+            }
+        }
+    }
+    return hit;
+}
+
+// Distance between two register images (candidate vs. an already kept candidate
+// of the same selection block): the value rows_dist gives for row b, query a.
+template <int G, int VM, typename T, int MET>
+__device__ __forceinline__ float reg_dist(const QReg<G, VM, T>& a, const QReg<G, VM, T>& b, int nchunks) {
+    constexpr int E = ChunkT<T>::E;
+    const int sl = lane_id() % G;
+    float acc = 0.f;
+#pragma unroll
+    for (int v = 0; v < VM; ++v) {
+        const bool live = (v * G + sl) < nchunks;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            float t;
+            if constexpr (MET == MET_L2) {
+                const float df = b.x[v][e] - a.x[v][e];
+                t = df * df;
+            } else {
+                t = b.x[v][e] * a.x[v][e];
+            }
+            acc += live ? t : 0.f;
+        }
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    return (MET == MET_L2) ? acc : 1.f - acc;
+}
+
 // ----------------------------------------------------------------- visited --
 
 struct Visited {

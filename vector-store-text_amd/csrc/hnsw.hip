@@ -111,16 +111,20 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
 // each candidate, in list order, against the block's earlier kept candidates
 // from registers -- the sequential decision for every candidate, with the same
 // distance values.  NQ = 2 halves the kept-row loads of one-at-a-time
-// (single: insert kernel +20 % time); NQ = 4 halves them again.
-#ifndef VSG_SEL_BLOCK
-#define VSG_SEL_BLOCK 4
+// (single: insert kernel +20 % time); NQ = 4 halves them again (C2 insert -1 %,
+// reverse -13 %; C4 shard insert -2 %, reverse -9 %).
+// NQ per row shape: up to 4 candidates, at most ~96 VGPRs of candidate images
+// (VM x E floats each: 24 for 768-d f32, 48 for 768-d f16, 8 for 128-d f16).
+#ifndef VSG_SEL_VGPRS
+#define VSG_SEL_VGPRS 96
 #endif
 #ifndef VSG_SEL_U
 #define VSG_SEL_U 1
 #endif
 template <int G, int VM, int U, typename T, int MET>
 __device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uint64_t& ndist) {
-    constexpr int NQ = VSG_SEL_BLOCK;
+    constexpr int QF = VM * ChunkT<T>::E;
+    constexpr int NQ = QF * 4 <= VSG_SEL_VGPRS ? 4 : QF * 3 <= VSG_SEL_VGPRS ? 3 : QF * 2 <= VSG_SEL_VGPRS ? 2 : 1;
     constexpr int UT = VSG_SEL_U < U ? VSG_SEL_U : U;  // row passes in flight per test
     constexpr int BLK = (64 / G) * UT;
     const int lane = lane_id();

@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--set", action="append", default=[])
-    ap.add_argument("--seeds", default="0", help="build mode: index seeds (offsets from the default)")
+    ap.add_argument("--seeds", default="0", help="index seeds (offsets from the default; search mode: the first)")
     ap.add_argument("--phases", action="store_true",
                     help="build mode, with VSG_LIB_PATH=lib_prof/libvsg.so (make prof): insert-wave "
                          "clock split into beam / heuristic selection")
@@ -135,7 +135,7 @@ def main():
             clear(env)
             del idx
         return
-    idx, bt = build(a, x)
+    idx, bt = build(a, x, int(a.seeds.split(",")[0]))
     del x
     gt = idx.search_device(qg, a.k, exact=True)[0].cpu().numpy()
     print(json.dumps(dict(head, build_s=round(bt, 3))), flush=True)

@@ -1,0 +1,58 @@
+"""GPU: the build's locality launch order changes no output.
+
+build_slots (vector-store-text_amd/csrc/vsg_index.cpp) launches the nodes of each
+insert batch grouped by locality cell (nearest of up to 1,024 pivot rows, found by the
+f32 MFMA exact kernel), dealt XCD-contiguously, so that co-resident waves insert
+neighbouring vectors and share rows in cache.  Nodes of one batch descend from the same
+graph snapshot, write only their own rows and their own pair range, and the pairs are
+sorted by (level, v, u) before the reverse-link kernel -- so the graph must be the same
+bit for bit with and without the reordering (VSG_BUILD_LOCALITY=0), for every metric,
+row width and for appends to a non-empty graph (f32 storage: f16 indexes keep the
+plain order).  The reference's add() is
+usearch's sequential insert (/root/reference/src/index/usearch.rs:221); parity of the
+batched build with it is covered by test_gpu_parity / test_gpu_c2_parity.
+"""
+import numpy as np
+import pytest
+
+import vsg
+from vsg import datagen as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _build(monkeypatch, locality, metric, quant, x, parts):
+    monkeypatch.setenv("VSG_BUILD_LOCALITY", locality)
+    monkeypatch.setenv("VSG_BUILD_LOCALITY_MIN", "256")  # small batches reorder too
+    idx = vsg.Index(x.shape[1], metric, quant, 16, 96, 64, seed=7)
+    lo = 0
+    for n in parts:
+        idx.add(np.arange(lo, lo + n), x[lo:lo + n])
+        lo += n
+    return idx
+
+
+@pytest.mark.parametrize("metric,quant,dim,data", [
+    ("cos", "f32", 768, "clustered"),
+    ("l2sq", "f32", 128, "sift"),
+    ("l2sq", "f16", 128, "sift"),
+    ("ip", "f32", 96, "clustered"),
+])
+def test_locality_order_same_graph(metric, quant, dim, data, monkeypatch):
+    n = 40_000
+    gen = G.sift_like if data == "sift" else G.clustered
+    x = gen(n, dim, 21, 22)
+    parts = (30_000, 10_000)  # a bulk build, then an append to the non-empty graph
+    a = _build(monkeypatch, "0", metric, quant, x, parts)
+    b = _build(monkeypatch, "1", metric, quant, x, parts)
+    ga, gb = a.export(), b.export()
+    assert (ga["entry"], ga["max_level"]) == (gb["entry"], gb["max_level"])
+    for f in ("levels", "adj0", "upper_off", "upper", "keys"):
+        np.testing.assert_array_equal(ga[f], gb[f], err_msg=f)
+    sa, sb = a.stats(), b.stats()
+    for f in ("build_distances", "build_adjacency", "build_batches"):
+        assert sa[f] == sb[f], f
+    q = gen(200, dim, 23, 22)
+    ma, mb = a.search(q, 10, 64), b.search(q, 10, 64)
+    np.testing.assert_array_equal(ma.keys, mb.keys)
+    np.testing.assert_array_equal(ma.distances, mb.distances)

@@ -32,7 +32,9 @@ sys.path.insert(0, os.path.join(ROOT, "vector-store-text_amd"))
 
 KNOBS = {"frac": "VSG_BUILD_BATCH_FRAC", "max": "VSG_BUILD_BATCH_MAX", "frac2": "VSG_BUILD_BATCH_FRAC2",
          "switch": "VSG_BUILD_BATCH_SWITCH", "reg": "VSG_SEARCH_REG", "waves": "VSG_SEARCH_WAVES",
-         "hash": "VSG_SEARCH_HASH_FACTOR", "xcd": "VSG_SEARCH_XCD_MAP", "upper": "VSG_SEARCH_UPPER_EF"}
+         "hash": "VSG_SEARCH_HASH_FACTOR", "xcd": "VSG_SEARCH_XCD_MAP", "upper": "VSG_SEARCH_UPPER_EF",
+         "loc": "VSG_BUILD_LOCALITY", "locmin": "VSG_BUILD_LOCALITY_MIN",
+         "piv": "VSG_BUILD_LOCALITY_PIVOTS"}
 
 
 def parse():
@@ -54,6 +56,9 @@ def parse():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--set", action="append", default=[])
+    ap.add_argument("--sort-base", action="store_true",
+                    help="build: rows inserted in synthetic-cluster order (slot ids spatial; probe of "
+                         "VSG_BUILD_LOCALITY=2)")
     ap.add_argument("--seeds", default="0", help="index seeds (offsets from the default; search mode: the first)")
     ap.add_argument("--phases", action="store_true",
                     help="build mode, with VSG_LIB_PATH=lib_prof/libvsg.so (make prof): insert-wave "
@@ -99,6 +104,10 @@ def main():
     bs, qs, ms = G.config_seeds(a.config)
     lo, hi = a.shard * a.rows // a.shards, (a.shard + 1) * a.rows // a.shards
     x = vsg.datagen_device(a.data, hi - lo, a.dim, bs, ms, start=lo)
+    if a.sort_base:
+        cl = (G.splitmix64(G._stream(bs, G.TAG_CLUSTER) + np.arange(lo, hi, dtype=np.uint64))
+              % np.uint64(G.N_CENTRES)).astype(np.int64)
+        x = x[torch.from_numpy(np.argsort(cl, kind="stable")).to(x.device)].contiguous()
     q = vsg.datagen_device(a.data, a.queries, a.dim, qs, ms)
     qg = q[: a.gt_queries].contiguous()
     per16 = 4 if a.quant == "f32" else 8

@@ -409,7 +409,11 @@ __global__ __launch_bounds__(64 * NW) void hnsw_search_wg_kernel(SearchParams p)
 template <int G, int VM, int U, typename T, int MET>
 __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int bi = blockIdx.x;
+    int bi = blockIdx.x;
+    if (p.perm) {  // sorted batch, dealt XCD-contiguously (block b runs on XCD b % 8)
+        const int n = p.nnodes, qd = n >> 3, rm = n & 7, x = blockIdx.x & 7, j = blockIdx.x >> 3;
+        bi = (int)p.perm[x * qd + min(x, rm) + j];
+    }
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
     WaveLds w = carve(smem, p.efc, p.hash_size, sel_entries(g.M0));

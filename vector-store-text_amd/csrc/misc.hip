@@ -132,6 +132,53 @@ hipError_t launch_gather_rows(const uint8_t* vecs, const float* sqnorm, const ui
     return hipGetLastError();
 }
 
+// ------------------------------------------------------- locality cells --
+// Build scheduling only (vsg_index.cpp build_slots): nearest pivot of each row
+// from the MFMA exact search's partial lists, and per-batch sort keys.
+
+__global__ void nearest_part_kernel(const float* __restrict__ part_d, const uint32_t* __restrict__ part_i, int nq,
+                                    int parts, int kin, uint32_t* __restrict__ out) {
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < nq; r += gridDim.x * blockDim.x) {
+        float bd = __builtin_inff();
+        uint32_t bi = 0;
+        const size_t base = (size_t)r * parts * kin;
+        for (int j = 0; j < parts * kin; ++j) {
+            const uint32_t id = part_i[base + j];
+            const float d = part_d[base + j];
+            if (id != 0xFFFFFFFFu && d < bd) {
+                bd = d;
+                bi = id;
+            }
+        }
+        out[r] = bi;
+    }
+}
+
+hipError_t launch_nearest_part(const float* part_d, const uint32_t* part_i, int nq, int parts, int kin,
+                               uint32_t* out, hipStream_t s) {
+    if (nq <= 0) return hipSuccess;
+    hipLaunchKernelGGL(nearest_part_kernel, dim3(capped_grid((size_t)nq, 256)), dim3(256), 0, s, part_d, part_i, nq,
+                       parts, kin, out);
+    return hipGetLastError();
+}
+
+__global__ void batch_keys_kernel(const uint32_t* __restrict__ nodes, int n, uint32_t s0,
+                                  const uint32_t* __restrict__ cell, uint64_t* __restrict__ okey,
+                                  uint32_t* __restrict__ oidx) {
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < n; b += gridDim.x * blockDim.x) {
+        okey[b] = ((uint64_t)cell[nodes[b] - s0] << 32) | (uint32_t)b;
+        oidx[b] = (uint32_t)b;
+    }
+}
+
+hipError_t launch_batch_keys(const uint32_t* nodes, int n, uint32_t s0, const uint32_t* cell, uint64_t* okey,
+                             uint32_t* oidx, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(batch_keys_kernel, dim3(capped_grid((size_t)n, 256)), dim3(256), 0, s, nodes, n, s0, cell,
+                       okey, oidx);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- datagen --
 // Same formulas and stream tags as vector-store-text_amd/vsg/datagen.py.
 

@@ -229,6 +229,17 @@ struct vsg_index {
     size_t sort_tmp_bytes = 0;
     float* d_stage = nullptr;
     size_t stage_cap = 0;  // rows
+    // locality launch order (build_slots, f32 rows): pivot rows, the call's cells,
+    // partial lists of the pivot search, per-batch sort keys
+    uint8_t* d_piv = nullptr;  // PIVOTS x row_bytes, then |row|^2, flags, slot ids, keys
+    uint32_t* d_cell = nullptr;
+    size_t cell_cap = 0;
+    float* d_cpart_d = nullptr;
+    uint32_t* d_cpart_i = nullptr;
+    size_t cpart_cap = 0;
+    uint64_t* d_okey[2] = {nullptr, nullptr};
+    uint32_t* d_oidx[2] = {nullptr, nullptr};
+    size_t border_cap = 0;
 
     // Locking (ABI: add/remove/search may be called concurrently, as the
     // reference does under its RwLock read side, src/index/usearch.rs:201-221, 276):
@@ -293,6 +304,14 @@ static void free_dev(vsg_index* h) {
     }
     hipFree(h->d_sort_tmp);
     hipFree(h->d_stage);
+    hipFree(h->d_piv);
+    hipFree(h->d_cell);
+    hipFree(h->d_cpart_d);
+    hipFree(h->d_cpart_i);
+    for (int i = 0; i < 2; ++i) {
+        hipFree(h->d_okey[i]);
+        hipFree(h->d_oidx[i]);
+    }
 }
 
 // grow a device array, copying `used` elements and filling the tail with `fill`
@@ -366,6 +385,118 @@ static int ensure_nodes(vsg_index* h, size_t n) {
     HIP_TRY(dev_alloc(&h->d_pair_off, want));
     HIP_TRY(dev_alloc(&h->d_bnodes, want));
     h->bnodes_cap = want;
+    return VSG_OK;
+}
+
+// ------------------------------------------------------- locality order --
+// The nodes of one insert batch all descend from the same graph snapshot, write
+// only their own rows and their own reverse-pair range (sorted by (level, v, u)
+// before the reverse kernel), so the order their waves launch in changes no
+// output.  It does change which rows co-resident waves share in cache: in a
+// random order every wave's efC beam fetches its own ~1,000 rows from HBM.
+// Launching a batch grouped by Voronoi cell (nearest of 1,024 pivot rows
+// sampled from the call, found by the f32 MFMA exact kernel) and dealt
+// XCD-contiguously (block b runs on XCD b % 8) makes the waves resident on one
+// XCD insert neighbouring vectors, whose beams share rows in its L2 and the
+// MALL.  f32 storage only (the MFMA kernel's row type).
+constexpr size_t LOC_PIVOTS = 4096, LOC_CHUNK = 262144;
+
+static int ensure_locality(vsg_index* h, size_t n, size_t max_b, size_t part_entries) {
+    if (!h->d_piv) HIP_TRY(dev_alloc(&h->d_piv, LOC_PIVOTS * (h->row_bytes + 4 + 1 + 4 + 8) + 256));
+    if (n > h->cell_cap) {
+        hipFree(h->d_cell);
+        h->d_cell = nullptr;
+        h->cell_cap = 0;
+        HIP_TRY(dev_alloc(&h->d_cell, std::max(n, h->cell_cap * 2)));
+        h->cell_cap = std::max(n, h->cell_cap * 2);
+    }
+    if (part_entries > h->cpart_cap) {
+        hipFree(h->d_cpart_d);
+        hipFree(h->d_cpart_i);
+        h->d_cpart_d = nullptr;
+        h->d_cpart_i = nullptr;
+        h->cpart_cap = 0;
+        HIP_TRY(dev_alloc(&h->d_cpart_d, part_entries));
+        HIP_TRY(dev_alloc(&h->d_cpart_i, part_entries));
+        h->cpart_cap = part_entries;
+    }
+    if (max_b > h->border_cap) {
+        for (int i = 0; i < 2; ++i) {
+            hipFree(h->d_okey[i]);
+            hipFree(h->d_oidx[i]);
+            h->d_okey[i] = nullptr;
+            h->d_oidx[i] = nullptr;
+        }
+        h->border_cap = 0;
+        for (int i = 0; i < 2; ++i) {
+            HIP_TRY(dev_alloc(&h->d_okey[i], max_b));
+            HIP_TRY(dev_alloc(&h->d_oidx[i], max_b));
+        }
+        h->border_cap = max_b;
+    }
+    return VSG_OK;
+}
+
+// MFMA exact-search shape for nq rows against np pivot rows (as the search path)
+struct CellShape {
+    int qtiles, splits, tps, nparts;
+};
+static CellShape cell_shape(size_t nq, size_t np) {
+    CellShape c;
+    c.qtiles = (int)((nq + MFMA_BQ - 1) / MFMA_BQ);
+    const size_t ntiles = (np + MFMA_BR - 1) / MFMA_BR;
+    size_t splits = std::min<size_t>(ntiles, std::max<size_t>(1, (1024 + c.qtiles - 1) / c.qtiles));
+    const size_t tps = (ntiles + splits - 1) / splits;
+    splits = (ntiles + tps - 1) / tps;
+    c.splits = (int)splits;
+    c.tps = (int)tps;
+    c.nparts = (int)splits * 4;
+    return c;
+}
+
+// d_cell[r] = nearest pivot of row s0 + r, r < n (stream-ordered; no host sync;
+// `idx` is the pivot slots' upload buffer and must outlive the stream's work)
+static int compute_cells(vsg_index* h, uint32_t s0, size_t n, std::vector<uint32_t>& idx, hipStream_t st) {
+    // pivot count (probe knob): 1,024 = the C2 build's best of 512 / 1,024 / 2,048
+    const size_t P = std::min({LOC_PIVOTS, n, (size_t)env_double("VSG_BUILD_LOCALITY_PIVOTS", 1024)});
+    size_t part_entries = 0;
+    for (size_t c0 = 0; c0 < n; c0 += LOC_CHUNK) {
+        const size_t nq = std::min(LOC_CHUNK, n - c0);
+        part_entries = std::max(part_entries, nq * (size_t)cell_shape(nq, P).nparts * 16);
+    }
+    int rc = ensure_locality(h, n, 0, part_entries);
+    if (rc) return rc;
+    uint8_t* pv = h->d_piv;
+    float* psq = reinterpret_cast<float*>(pv + LOC_PIVOTS * h->row_bytes);
+    uint8_t* pflags = reinterpret_cast<uint8_t*>(psq + LOC_PIVOTS);
+    uint32_t* pidx = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(pflags + LOC_PIVOTS) + 15) & ~(uintptr_t)15);
+    uint64_t* pkeys = reinterpret_cast<uint64_t*>(pidx + LOC_PIVOTS);
+    idx.resize(P);
+    for (size_t i = 0; i < P; ++i) idx[i] = s0 + (uint32_t)(i * n / P);
+    HIP_TRY(hipMemcpyAsync(pidx, idx.data(), P * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(pflags, 0, P, st));
+    HIP_TRY(launch_gather_rows(h->d_vecs, h->d_sqnorm, h->d_keys, pidx, P, h->row_bytes, pv, psq, pkeys, st));
+    for (size_t c0 = 0; c0 < n; c0 += LOC_CHUNK) {
+        const size_t nq = std::min(LOC_CHUNK, n - c0);
+        const CellShape cs = cell_shape(nq, P);
+        MfmaExactParams mp{};
+        mp.vecs = reinterpret_cast<const float*>(pv);
+        mp.sqnorm = psq;
+        mp.queries = reinterpret_cast<const float*>(h->d_vecs + (size_t)(s0 + c0) * h->row_bytes);
+        mp.qsqnorm = h->d_sqnorm + s0 + c0;
+        mp.row_floats = (int)(h->row_bytes / 4);
+        mp.nq = (int)nq;
+        mp.nslots = P;
+        mp.flags = pflags;
+        mp.qtiles = cs.qtiles;
+        mp.splits = cs.splits;
+        mp.tiles_per_split = cs.tps;
+        mp.kmax = 16;
+        mp.part_d = h->d_cpart_d;
+        mp.part_i = h->d_cpart_i;
+        HIP_TRY(launch_mfma_exact(h->mk, mp, st));
+        HIP_TRY(launch_nearest_part(h->d_cpart_d, h->d_cpart_i, (int)nq, cs.nparts, 16, h->d_cell + c0, st));
+    }
     return VSG_OK;
 }
 
@@ -464,6 +595,14 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     // VSG_BUILD_PERMUTE: 0 slot order (sequential-build identity tests), 2 serial
     // Fisher-Yates (round 1's order; probes)
     const int pmode = (int)env_double("VSG_BUILD_PERMUTE", 1);
+    // Launch order of a batch's nodes: grouped by locality cell for batches of
+    // >= lmin nodes (VSG_BUILD_LOCALITY=0: the permutation's order).  The cells
+    // are computed on the device while the host plans.
+    const size_t lmin = (size_t)env_double("VSG_BUILD_LOCALITY_MIN", 4096);
+    const bool locality = env_double("VSG_BUILD_LOCALITY", 1) != 0 && h->st == ST_F32 &&
+                          (h->row_bytes / 4) % 32 == 0 && n >= 2 * lmin;
+    std::vector<uint32_t> piv_idx;
+    if (locality && (rc = compute_cells(h, s0, n, piv_idx, st))) return rc;
     const uint64_t pkey = host_splitmix64(h->opt.seed ^ 0x5045524D55544Eull ^ (uint64_t)s0);
     const SlotPerm perm(n, pkey);
     if (pmode == 2) {
@@ -485,6 +624,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         uint32_t entry;  // entry point / top level the batch descends from
         int max_level;
         int new_top;  // > max_level: the batch's last node becomes the entry
+        uint32_t top_node;  // that node
     };
     // batch = frac x graph size, at most bmax (and at least 8 batches per call).
     // Round 2 sweep at C2 (profiles/r02_build_schedule.jsonl, recall@10 on 10k
@@ -530,7 +670,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
                 pair_off[i + j] = acc;
                 acc += (uint32_t)(h->M0 + std::min<int>(blev[i + j], maxl) * h->M);
             }
-            plan.push_back({i, b, (size_t)acc, entry, maxl, new_top});
+            plan.push_back({i, b, (size_t)acc, entry, maxl, new_top, order[i + b - 1]});
             max_pairs = std::max<size_t>(max_pairs, acc);
             if (new_top >= 0) {
                 entry = order[i + b - 1];
@@ -542,6 +682,11 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
             h->entry = entry;
             h->max_level = maxl;
         }
+    }
+    if (locality) {
+        size_t max_b = 0;
+        for (const Batch& B : plan) max_b = std::max(max_b, B.b);
+        if ((rc = ensure_locality(h, n, max_b, 0))) return rc;
     }
     if ((rc = ensure_pairs(h, max_pairs))) return rc;
     {
@@ -588,6 +733,12 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         ip.hash_size = hash;
         ip.stats = h->d_stats;
         HIP_TRY(hipEventRecord(ev[0], st));
+        if (locality && B.b >= lmin) {  // see ensure_locality: same graph, fewer HBM reads
+            HIP_TRY(launch_batch_keys(h->d_bnodes + B.i, (int)B.b, s0, h->d_cell, h->d_okey[0], h->d_oidx[0], st));
+            size_t otmp = h->sort_tmp_bytes;
+            HIP_TRY(sort_pairs(h->d_sort_tmp, otmp, h->d_okey[0], h->d_okey[1], h->d_oidx[0], h->d_oidx[1], B.b, st));
+            ip.perm = h->d_oidx[1];
+        }
         HIP_TRY(launch_insert(h->st, h->mk, ip, st));
         HIP_TRY(hipEventRecord(ev[1], st));
         size_t tmp = h->sort_tmp_bytes;
@@ -603,7 +754,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         HIP_TRY(launch_reverse(h->st, h->mk, rp, grid, st));
         HIP_TRY(hipEventRecord(ev[3], st));
         if (B.new_top >= 0) {
-            h->entry = order[B.i + B.b - 1];
+            h->entry = B.top_node;
             h->max_level = B.new_top;
         } else {
             h->entry = B.entry;

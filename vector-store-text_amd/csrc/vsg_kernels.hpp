@@ -51,6 +51,9 @@ struct InsertParams {
     int efc;
     int hash_size;              // visited-table entries (hash_size_for)
     unsigned long long* stats;  // [3] n_dist, [4] n_adj, [5] selection
+    // Locality launch order (vsg_index.cpp build_slots): block b inserts batch
+    // node perm[xcd_pos(b)] (nullptr: node b)
+    const uint32_t* perm;
 };
 
 struct ReverseParams {
@@ -165,6 +168,13 @@ hipError_t launch_set_flags(uint8_t* flags, const uint32_t* slots, size_t n, uin
 hipError_t launch_gather_rows(const uint8_t* vecs, const float* sqnorm, const uint64_t* keys,
                               const uint32_t* idx, size_t n, size_t row_bytes, uint8_t* out_vecs,
                               float* out_sq, uint64_t* out_keys, hipStream_t s);
+// locality cells (build launch order): out[r] = the nearest of the partial-list
+// entries of row r (MFMA exact search of the rows against pivot rows)
+hipError_t launch_nearest_part(const float* part_d, const uint32_t* part_i, int nq, int parts, int kin,
+                               uint32_t* out, hipStream_t s);
+// okey[b] = cell[nodes[b] - s0] << 32 | b, oidx[b] = b for the n nodes of one batch
+hipError_t launch_batch_keys(const uint32_t* nodes, int n, uint32_t s0, const uint32_t* cell, uint64_t* okey,
+                             uint32_t* oidx, hipStream_t s);
 hipError_t launch_datagen(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed,
                           size_t start_row, float* out, float* scratch_w, float* scratch_c,
                           hipStream_t s);

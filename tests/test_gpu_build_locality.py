@@ -7,8 +7,8 @@ neighbouring vectors and share rows in cache.  Nodes of one batch descend from t
 graph snapshot, write only their own rows and their own pair range, and the pairs are
 sorted by (level, v, u) before the reverse-link kernel -- so the graph must be the same
 bit for bit with and without the reordering (VSG_BUILD_LOCALITY=0), for every metric,
-row width and for appends to a non-empty graph (f32 storage: f16 indexes keep the
-plain order).  The reference's add() is
+row width, f32 and f16 storage (f16 rows widened chunk by chunk for the MFMA kernel)
+and for appends to a non-empty graph.  The reference's add() is
 usearch's sequential insert (/root/reference/src/index/usearch.rs:221); parity of the
 batched build with it is covered by test_gpu_parity / test_gpu_c2_parity.
 """

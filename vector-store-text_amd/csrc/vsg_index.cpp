@@ -234,6 +234,7 @@ struct vsg_index {
     uint8_t* d_piv = nullptr;  // PIVOTS x row_bytes, then |row|^2, flags, slot ids, keys
     uint32_t* d_cell = nullptr;
     size_t cell_cap = 0;
+    float* d_cf32 = nullptr;  // f16 storage: one chunk of rows widened to f32 for the MFMA kernel
     float* d_cpart_d = nullptr;
     uint32_t* d_cpart_i = nullptr;
     size_t cpart_cap = 0;
@@ -306,6 +307,7 @@ static void free_dev(vsg_index* h) {
     hipFree(h->d_stage);
     hipFree(h->d_piv);
     hipFree(h->d_cell);
+    hipFree(h->d_cf32);
     hipFree(h->d_cpart_d);
     hipFree(h->d_cpart_i);
     for (int i = 0; i < 2; ++i) {
@@ -398,17 +400,23 @@ static int ensure_nodes(vsg_index* h, size_t n) {
 // sampled from the call, found by the f32 MFMA exact kernel) and dealt
 // XCD-contiguously (block b runs on XCD b % 8) makes the waves resident on one
 // XCD insert neighbouring vectors, whose beams share rows in its L2 and the
-// MALL.  f32 storage only (the MFMA kernel's row type).
+// MALL.  The MFMA kernel reads f32 rows: f16 rows are widened chunk by chunk.
 constexpr size_t LOC_PIVOTS = 4096, LOC_CHUNK = 262144;
 
+// f32 elements per row as the MFMA kernel sees it (the padded storage row)
+static size_t loc_row_floats(const vsg_index* h) { return h->st == ST_F32 ? h->row_bytes / 4 : h->row_bytes / 2; }
+
 static int ensure_locality(vsg_index* h, size_t n, size_t max_b, size_t part_entries) {
-    if (!h->d_piv) HIP_TRY(dev_alloc(&h->d_piv, LOC_PIVOTS * (h->row_bytes + 4 + 1 + 4 + 8) + 256));
+    const size_t rf = loc_row_floats(h);
+    if (!h->d_piv) HIP_TRY(dev_alloc(&h->d_piv, LOC_PIVOTS * (rf * 4 + 4 + 1 + 4 + 8) + 256));
+    if (h->st == ST_F16 && !h->d_cf32) HIP_TRY(dev_alloc(&h->d_cf32, LOC_CHUNK * rf));
     if (n > h->cell_cap) {
+        const size_t want = std::max(n, h->cell_cap * 2);
         hipFree(h->d_cell);
         h->d_cell = nullptr;
         h->cell_cap = 0;
-        HIP_TRY(dev_alloc(&h->d_cell, std::max(n, h->cell_cap * 2)));
-        h->cell_cap = std::max(n, h->cell_cap * 2);
+        HIP_TRY(dev_alloc(&h->d_cell, want));
+        h->cell_cap = want;
     }
     if (part_entries > h->cpart_cap) {
         hipFree(h->d_cpart_d);
@@ -454,6 +462,38 @@ static CellShape cell_shape(size_t nq, size_t np) {
     return c;
 }
 
+struct PivotView {
+    uint8_t* rows;
+    float* sq;
+    uint8_t* flags;
+    uint32_t* idx;
+    uint64_t* keys;
+};
+static PivotView pivot_view(vsg_index* h) {
+    PivotView v;
+    v.rows = h->d_piv;
+    v.sq = reinterpret_cast<float*>(v.rows + LOC_PIVOTS * loc_row_floats(h) * 4);
+    v.flags = reinterpret_cast<uint8_t*>(v.sq + LOC_PIVOTS);
+    v.idx = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(v.flags + LOC_PIVOTS) + 15) & ~(uintptr_t)15);
+    v.keys = reinterpret_cast<uint64_t*>(v.idx + LOC_PIVOTS);
+    return v;
+}
+
+// cells of nq prepared f32 rows (`rows`, |row|^2 in `sq` for L2) against the np
+// pivots: out[r] = the nearest pivot (MFMA exact top-16 partial lists in
+// part_d / part_i, then the nearest entry)
+static hipError_t rows_to_cells(vsg_index* h, const uint8_t* rows, const float* sq, size_t nq, size_t np,
+                                float* part_d, uint32_t* part_i, uint32_t* out, hipStream_t st);
+
+// rows [s0 + c0, s0 + c0 + nq) as the MFMA kernel reads them: the storage rows
+// themselves (f32), or widened into the chunk buffer (f16)
+static const uint8_t* loc_rows(vsg_index* h, size_t first, size_t nq, hipStream_t st, hipError_t& e) {
+    const uint8_t* src = h->d_vecs + first * h->row_bytes;
+    if (h->st == ST_F32) return src;
+    e = launch_unprepare(ST_F16, src, nq, (int)loc_row_floats(h), h->row_bytes, h->d_cf32, st);
+    return reinterpret_cast<const uint8_t*>(h->d_cf32);
+}
+
 // d_cell[r] = nearest pivot of row s0 + r, r < n (stream-ordered; no host sync;
 // `idx` is the pivot slots' upload buffer and must outlive the stream's work)
 static int compute_cells(vsg_index* h, uint32_t s0, size_t n, std::vector<uint32_t>& idx, hipStream_t st) {
@@ -466,38 +506,53 @@ static int compute_cells(vsg_index* h, uint32_t s0, size_t n, std::vector<uint32
     }
     int rc = ensure_locality(h, n, 0, part_entries);
     if (rc) return rc;
-    uint8_t* pv = h->d_piv;
-    float* psq = reinterpret_cast<float*>(pv + LOC_PIVOTS * h->row_bytes);
-    uint8_t* pflags = reinterpret_cast<uint8_t*>(psq + LOC_PIVOTS);
-    uint32_t* pidx = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(pflags + LOC_PIVOTS) + 15) & ~(uintptr_t)15);
-    uint64_t* pkeys = reinterpret_cast<uint64_t*>(pidx + LOC_PIVOTS);
+    const PivotView pv = pivot_view(h);
     idx.resize(P);
     for (size_t i = 0; i < P; ++i) idx[i] = s0 + (uint32_t)(i * n / P);
-    HIP_TRY(hipMemcpyAsync(pidx, idx.data(), P * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(pflags, 0, P, st));
-    HIP_TRY(launch_gather_rows(h->d_vecs, h->d_sqnorm, h->d_keys, pidx, P, h->row_bytes, pv, psq, pkeys, st));
+    HIP_TRY(hipMemcpyAsync(pv.idx, idx.data(), P * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(pv.flags, 0, P, st));
+    if (h->st == ST_F32) {
+        HIP_TRY(launch_gather_rows(h->d_vecs, h->d_sqnorm, h->d_keys, pv.idx, P, h->row_bytes, pv.rows, pv.sq,
+                                   pv.keys, st));
+    } else {  // gather f16 rows into the chunk buffer, widen into the pivot rows
+        uint8_t* tmp = reinterpret_cast<uint8_t*>(h->d_cf32);
+        HIP_TRY(launch_gather_rows(h->d_vecs, h->d_sqnorm, h->d_keys, pv.idx, P, h->row_bytes, tmp, pv.sq, pv.keys,
+                                   st));
+        HIP_TRY(launch_unprepare(ST_F16, tmp, P, (int)loc_row_floats(h), h->row_bytes,
+                                 reinterpret_cast<float*>(pv.rows), st));
+    }
     for (size_t c0 = 0; c0 < n; c0 += LOC_CHUNK) {
         const size_t nq = std::min(LOC_CHUNK, n - c0);
-        const CellShape cs = cell_shape(nq, P);
-        MfmaExactParams mp{};
-        mp.vecs = reinterpret_cast<const float*>(pv);
-        mp.sqnorm = psq;
-        mp.queries = reinterpret_cast<const float*>(h->d_vecs + (size_t)(s0 + c0) * h->row_bytes);
-        mp.qsqnorm = h->d_sqnorm + s0 + c0;
-        mp.row_floats = (int)(h->row_bytes / 4);
-        mp.nq = (int)nq;
-        mp.nslots = P;
-        mp.flags = pflags;
-        mp.qtiles = cs.qtiles;
-        mp.splits = cs.splits;
-        mp.tiles_per_split = cs.tps;
-        mp.kmax = 16;
-        mp.part_d = h->d_cpart_d;
-        mp.part_i = h->d_cpart_i;
-        HIP_TRY(launch_mfma_exact(h->mk, mp, st));
-        HIP_TRY(launch_nearest_part(h->d_cpart_d, h->d_cpart_i, (int)nq, cs.nparts, 16, h->d_cell + c0, st));
+        hipError_t e = hipSuccess;
+        const uint8_t* rows = loc_rows(h, (size_t)s0 + c0, nq, st, e);
+        HIP_TRY(e);
+        HIP_TRY(rows_to_cells(h, rows, h->d_sqnorm + s0 + c0, nq, P, h->d_cpart_d, h->d_cpart_i, h->d_cell + c0, st));
     }
     return VSG_OK;
+}
+
+static hipError_t rows_to_cells(vsg_index* h, const uint8_t* rows, const float* sq, size_t nq, size_t np,
+                                float* part_d, uint32_t* part_i, uint32_t* out, hipStream_t st) {
+    const PivotView pv = pivot_view(h);
+    const CellShape cs = cell_shape(nq, np);
+    MfmaExactParams mp{};
+    mp.vecs = reinterpret_cast<const float*>(pv.rows);
+    mp.sqnorm = pv.sq;
+    mp.queries = reinterpret_cast<const float*>(rows);
+    mp.qsqnorm = sq;
+    mp.row_floats = (int)loc_row_floats(h);
+    mp.nq = (int)nq;
+    mp.nslots = np;
+    mp.flags = pv.flags;
+    mp.qtiles = cs.qtiles;
+    mp.splits = cs.splits;
+    mp.tiles_per_split = cs.tps;
+    mp.kmax = 16;
+    mp.part_d = part_d;
+    mp.part_i = part_i;
+    hipError_t e = launch_mfma_exact(h->mk, mp, st);
+    if (e == hipSuccess) e = launch_nearest_part(part_d, part_i, (int)nq, cs.nparts, 16, out, st);
+    return e;
 }
 
 static int ensure_pairs(vsg_index* h, size_t n) {
@@ -599,8 +654,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     // >= lmin nodes (VSG_BUILD_LOCALITY=0: the permutation's order).  The cells
     // are computed on the device while the host plans.
     const size_t lmin = (size_t)env_double("VSG_BUILD_LOCALITY_MIN", 4096);
-    const bool locality = env_double("VSG_BUILD_LOCALITY", 1) != 0 && h->st == ST_F32 &&
-                          (h->row_bytes / 4) % 32 == 0 && n >= 2 * lmin;
+    const bool locality = env_double("VSG_BUILD_LOCALITY", 1) != 0 && loc_row_floats(h) % 32 == 0 && n >= 2 * lmin;
     std::vector<uint32_t> piv_idx;
     if (locality && (rc = compute_cells(h, s0, n, piv_idx, st))) return rc;
     const uint64_t pkey = host_splitmix64(h->opt.seed ^ 0x5045524D55544Eull ^ (uint64_t)s0);
@@ -1214,7 +1268,7 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
     float* cd = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(ck) + align256(nq * efr * 8));
     uint32_t* cc = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(cd) + align256(nq * efr * 4));
     uint8_t* qp = ws->base;
-    float* qsq = use_mfma ? reinterpret_cast<float*>(ws->base + qp_b) : nullptr;
+    float* qsq = qsq_b ? reinterpret_cast<float*>(ws->base + qp_b) : nullptr;
     float* pd = reinterpret_cast<float*>(ws->base + qp_b + qsq_b);
     uint32_t* pi = reinterpret_cast<uint32_t*>(ws->base + qp_b + qsq_b + part_b);
     hipError_t err = launch_prepare(h->st, q_dev, nq, h->dim, h->normalize, qp, h->row_bytes, s, qsq);

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstddef>
 #include <cstdio>
@@ -137,6 +138,24 @@ double env_double(const char* name, double dflt) {
     const char* v = getenv(name);
     return v && *v ? atof(v) : dflt;
 }
+
+// VSG_DEBUG_TIMING=1: host-side phase times of an add, to stderr (probes only)
+struct PhaseClock {
+    bool on = env_double("VSG_DEBUG_TIMING", 0) != 0;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    std::string line;
+    void mark(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        char buf[64];
+        snprintf(buf, sizeof buf, " %s=%.2fms", what, std::chrono::duration<double, std::milli>(now - t).count());
+        line += buf;
+        t = now;
+    }
+    ~PhaseClock() {
+        if (on && !line.empty()) fprintf(stderr, "[vsg timing]%s\n", line.c_str());
+    }
+};
 
 }  // namespace
 
@@ -642,6 +661,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         return VSG_OK;
     }
     if ((rc = ensure_nodes(h, n))) return rc;
+    PhaseClock pc;
     // Insertion order = a seeded pseudo-random permutation of the call's slots:
     // nodes of one batch cannot link to each other, so a batch must not be
     // spatially coherent (a cluster-sorted input otherwise wrecks the graph).
@@ -657,6 +677,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     const bool locality = env_double("VSG_BUILD_LOCALITY", 1) != 0 && loc_row_floats(h) % 32 == 0 && n >= 2 * lmin;
     std::vector<uint32_t> piv_idx;
     if (locality && (rc = compute_cells(h, s0, n, piv_idx, st))) return rc;
+    pc.mark("b:cells_enqueue");
     const uint64_t pkey = host_splitmix64(h->opt.seed ^ 0x5045524D55544Eull ^ (uint64_t)s0);
     const SlotPerm perm(n, pkey);
     if (pmode == 2) {
@@ -737,6 +758,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
             h->max_level = maxl;
         }
     }
+    pc.mark("b:order+plan");
     if (locality) {
         size_t max_b = 0;
         for (const Batch& B : plan) max_b = std::max(max_b, B.b);
@@ -762,6 +784,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     HIP_TRY(hipMemcpyAsync(h->d_bnodes, order.data(), n * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_blevels, blev.data(), n, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_pair_off, pair_off.data(), n * 4, hipMemcpyHostToDevice, st));
+    pc.mark("b:buffers+uploads");
 
     // pairs per reverse-kernel wave: with batches of up to 64k nodes, 64 pairs a
     // wave beat 16 (round 1's choice for 1/16-graph batches): C2 reverse 0.120 ->
@@ -817,8 +840,10 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         h->build_batches++;
     }
     h->build_vectors += n;
+    pc.mark("b:enqueue_batches");
     if (!plan.empty()) {
         HIP_TRY(hipStreamSynchronize(st));
+        pc.mark("b:device_drain");
         for (size_t bi = 0; bi < plan.size(); ++bi) {
             float t[3] = {0.f, 0.f, 0.f};
             for (int j = 0; j < 3; ++j)
@@ -1036,6 +1061,7 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
     if (n == 0) return VSG_OK;
     std::lock_guard<std::mutex> wl(h->wmu);
     DeviceGuard dg(h->device);
+    PhaseClock pc;
     int rc;
     uint32_t s0;
     {
@@ -1047,18 +1073,24 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
             if ((rc = reserve_locked(h, std::min<size_t>(want, MAX_SLOTS)))) return rc;
         }
         s0 = (uint32_t)h->slots;
+        pc.mark("lock+reserve");
         if ((rc = map_keys(h, keys, n, s0))) return rc;
+        pc.mark("map_keys");
         if ((rc = stage_slots(h, s0, n, keys))) {
             unmap_keys(h, keys, n);
             return rc;
         }
+        pc.mark("stage");
     }
     rc = put_rows(h, vecs, n, device_src, user_stream, s0);
+    pc.mark("put_rows");
     if (rc == VSG_OK) rc = build_slots(h, s0, n);
+    pc.mark("build_slots");
     if (rc == VSG_OK) {
         const hipError_t e = hipStreamSynchronize(h->stream);
         if (e != hipSuccess) rc = fail(VSG_EDEVICE, std::string("add: ") + hipGetErrorString(e));
     }
+    pc.mark("sync");
     std::unique_lock<std::shared_mutex> lk(h->mu);
     if (rc) {
         // Roll back: the keys leave the map, live is unchanged.  The staged rows

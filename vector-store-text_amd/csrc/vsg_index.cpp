@@ -254,6 +254,7 @@ struct vsg_index {
     uint32_t* d_cell = nullptr;
     size_t cell_cap = 0;
     float* d_cf32 = nullptr;  // f16 storage: one chunk of rows widened to f32 for the MFMA kernel
+    size_t cf32_cap = 0;      // rows
     float* d_cpart_d = nullptr;
     uint32_t* d_cpart_i = nullptr;
     size_t cpart_cap = 0;
@@ -425,10 +426,24 @@ constexpr size_t LOC_PIVOTS = 4096, LOC_CHUNK = 262144;
 // f32 elements per row as the MFMA kernel sees it (the padded storage row)
 static size_t loc_row_floats(const vsg_index* h) { return h->st == ST_F32 ? h->row_bytes / 4 : h->row_bytes / 2; }
 
-static int ensure_locality(vsg_index* h, size_t n, size_t max_b, size_t part_entries) {
+// rows per cell launch: the MFMA kernel's partial lists (nq x parts x 16 x 8 B,
+// ~134 MB at 256k rows) and, for f16 rows, the widened chunk (capped at 128 MB)
+static size_t loc_chunk(const vsg_index* h, size_t n) {
+    size_t c = LOC_CHUNK;
+    if (h->st == ST_F16) c = std::min(c, std::max(LOC_PIVOTS, ((size_t)32 << 20) / loc_row_floats(h)));
+    return std::min(c, n);
+}
+
+static int ensure_locality(vsg_index* h, size_t n, size_t max_b, size_t part_entries, size_t chunk = 0) {
     const size_t rf = loc_row_floats(h);
     if (!h->d_piv) HIP_TRY(dev_alloc(&h->d_piv, LOC_PIVOTS * (rf * 4 + 4 + 1 + 4 + 8) + 256));
-    if (h->st == ST_F16 && !h->d_cf32) HIP_TRY(dev_alloc(&h->d_cf32, LOC_CHUNK * rf));
+    if (h->st == ST_F16 && chunk > h->cf32_cap) {
+        hipFree(h->d_cf32);
+        h->d_cf32 = nullptr;
+        h->cf32_cap = 0;
+        HIP_TRY(dev_alloc(&h->d_cf32, chunk * rf));
+        h->cf32_cap = chunk;
+    }
     if (n > h->cell_cap) {
         const size_t want = std::max(n, h->cell_cap * 2);
         hipFree(h->d_cell);
@@ -518,12 +533,14 @@ static const uint8_t* loc_rows(vsg_index* h, size_t first, size_t nq, hipStream_
 static int compute_cells(vsg_index* h, uint32_t s0, size_t n, std::vector<uint32_t>& idx, hipStream_t st) {
     // pivot count (probe knob): 1,024 = the C2 build's best of 512 / 1,024 / 2,048
     const size_t P = std::min({LOC_PIVOTS, n, (size_t)env_double("VSG_BUILD_LOCALITY_PIVOTS", 1024)});
+    // the f16 pivot rows are staged in the widened-chunk buffer: chunk >= P
+    const size_t chunk = std::max(loc_chunk(h, n), P);
     size_t part_entries = 0;
-    for (size_t c0 = 0; c0 < n; c0 += LOC_CHUNK) {
-        const size_t nq = std::min(LOC_CHUNK, n - c0);
+    for (size_t c0 = 0; c0 < n; c0 += chunk) {
+        const size_t nq = std::min(chunk, n - c0);
         part_entries = std::max(part_entries, nq * (size_t)cell_shape(nq, P).nparts * 16);
     }
-    int rc = ensure_locality(h, n, 0, part_entries);
+    int rc = ensure_locality(h, n, 0, part_entries, chunk);
     if (rc) return rc;
     const PivotView pv = pivot_view(h);
     idx.resize(P);
@@ -540,8 +557,8 @@ static int compute_cells(vsg_index* h, uint32_t s0, size_t n, std::vector<uint32
         HIP_TRY(launch_unprepare(ST_F16, tmp, P, (int)loc_row_floats(h), h->row_bytes,
                                  reinterpret_cast<float*>(pv.rows), st));
     }
-    for (size_t c0 = 0; c0 < n; c0 += LOC_CHUNK) {
-        const size_t nq = std::min(LOC_CHUNK, n - c0);
+    for (size_t c0 = 0; c0 < n; c0 += chunk) {
+        const size_t nq = std::min(chunk, n - c0);
         hipError_t e = hipSuccess;
         const uint8_t* rows = loc_rows(h, (size_t)s0 + c0, nq, st, e);
         HIP_TRY(e);

@@ -56,3 +56,32 @@ def test_locality_order_same_graph(metric, quant, dim, data, monkeypatch):
     ma, mb = a.search(q, 10, 64), b.search(q, 10, 64)
     np.testing.assert_array_equal(ma.keys, mb.keys)
     np.testing.assert_array_equal(ma.distances, mb.distances)
+
+
+@pytest.mark.parametrize("metric,quant,dim,M,efc", [
+    ("cos", "f32", 768, 16, 128),
+    ("l2sq", "f16", 128, 16, 192),
+    ("ip", "f32", 96, 48, 64),
+])
+def test_split_insert_same_graph(metric, quant, dim, M, efc, monkeypatch):
+    """The insert as two launches (beam kernel -> lists in HBM -> selection kernel,
+    csrc/hnsw.hip hnsw_insert_beam_kernel / hnsw_insert_select_kernel) builds the
+    graph of the fused hnsw_insert_kernel bit for bit (VSG_BUILD_SPLIT=0)."""
+    n = 30_000
+    x = (G.sift_like if quant == "f16" else G.clustered)(n, dim, 61, 62)
+
+    def build(split):
+        monkeypatch.setenv("VSG_BUILD_SPLIT", split)
+        idx = vsg.Index(dim, metric, quant, M, efc, 64, seed=8)
+        idx.add(np.arange(20_000), x[:20_000])
+        idx.add(np.arange(20_000, n), x[20_000:])
+        return idx
+
+    a, b = build("0"), build("1")
+    ga, gb = a.export(), b.export()
+    assert (ga["entry"], ga["max_level"]) == (gb["entry"], gb["max_level"])
+    for f in ("levels", "adj0", "upper_off", "upper"):
+        np.testing.assert_array_equal(ga[f], gb[f], err_msg=f)
+    sa, sb = a.stats(), b.stats()
+    for f in ("build_distances", "build_adjacency", "build_select_distances"):
+        assert sa[f] == sb[f], f

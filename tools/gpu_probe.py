@@ -34,7 +34,8 @@ KNOBS = {"frac": "VSG_BUILD_BATCH_FRAC", "max": "VSG_BUILD_BATCH_MAX", "frac2": 
          "switch": "VSG_BUILD_BATCH_SWITCH", "reg": "VSG_SEARCH_REG", "waves": "VSG_SEARCH_WAVES",
          "hash": "VSG_SEARCH_HASH_FACTOR", "xcd": "VSG_SEARCH_XCD_MAP", "upper": "VSG_SEARCH_UPPER_EF",
          "loc": "VSG_BUILD_LOCALITY", "locmin": "VSG_BUILD_LOCALITY_MIN",
-         "piv": "VSG_BUILD_LOCALITY_PIVOTS"}
+         "piv": "VSG_BUILD_LOCALITY_PIVOTS",
+         "split": "VSG_BUILD_SPLIT", "bhash": "VSG_BUILD_HASH_FACTOR"}
 
 
 def parse():

@@ -474,6 +474,108 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     }
 }
 
+// ------------------------------------------------------------ build: split --
+// The insert kernel above in two launches.  Its register footprint is set by the
+// heuristic selection (NQ candidate images + row loads: 232 VGPRs at C2, 2
+// waves/SIMD) while 2/3 of its time is the efC beam, which needs about half.
+// hnsw_insert_beam_kernel runs descent + beam of every level at the beam's own
+// occupancy and stores each level's sorted top-efc list (as regset_to_list
+// leaves it in LDS) in HBM; hnsw_insert_select_kernel reloads the lists and runs
+// the selection, row writes and pair emission in the same level order.  Same
+// operations on the same values: the graph is bit-identical to the fused kernel.
+
+__device__ __forceinline__ int insert_index(const InsertParams& p) {
+    if (!p.perm) return blockIdx.x;
+    const int n = p.nnodes, qd = n >> 3, rm = n & 7, x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    return (int)p.perm[x * qd + min(x, rm) + j];
+}
+
+template <int G, int VM, int U, typename T, int MET>
+__global__ __launch_bounds__(64) void hnsw_insert_beam_kernel(InsertParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int bi = insert_index(p);
+    const int lane = lane_id();
+    const GraphDev g = to_dev(p.g);
+    WaveLds w = carve(smem, p.efc, p.hash_size, 0);
+    const uint64_t t_start = wall_clock64();
+    const uint32_t node = p.nodes[bi];
+    const int L = p.levels[bi];
+    uint64_t ndist = 0, nadj = 0;
+    BeamProf pf;
+    QReg<G, VM, T> q;
+    q.load(g.vec(node), g.nchunks);
+    uint32_t cur = p.entry;
+    float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
+    ++ndist;
+    for (int l = p.max_level; l > L; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+    for (int l = min(L, p.max_level); l >= 0; --l) {
+        RegSet<4> B;
+        beam_reg<G, VM, U, T, MET, 4>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf);
+        regset_to_list<4>(B, p.efc, w);
+        const size_t slot = (size_t)p.list_off[bi] + (size_t)l;
+        const int n = w.list.size;
+        float* od = p.lst_d + slot * (size_t)p.efc;
+        uint32_t* oi = p.lst_i + slot * (size_t)p.efc;
+        for (int j = lane; j < n; j += 64) {
+            od[j] = w.list.d0[j];
+            oi[j] = w.list.i0[j];
+        }
+        if (lane == 0) p.lst_n[slot] = n;
+        cur = w.list.i0[0] & VSG_ID_MASK;
+        dcur = w.list.d0[0];
+        wave_sync();
+    }
+    if (lane == 0 && p.stats) {
+        atomicAdd(&p.stats[3], (unsigned long long)ndist);
+        atomicAdd(&p.stats[4], (unsigned long long)nadj);
+        const unsigned long long dt = wall_clock64() - t_start;
+        atomicAdd(&p.stats[10], dt);
+        atomicMax(&p.stats[11], dt);
+    }
+}
+
+template <int G, int VM, int U, typename T, int MET>
+__global__ __launch_bounds__(64) void hnsw_insert_select_kernel(InsertParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int bi = insert_index(p);
+    const int lane = lane_id();
+    const GraphDev g = to_dev(p.g);
+    WaveLds w = carve(smem, p.efc, 0, sel_entries(g.M0));
+    const uint32_t node = p.nodes[bi];
+    const int L = p.levels[bi];
+    uint64_t nsel_d = 0;
+    uint32_t pos = p.pair_off[bi];
+    for (int l = min(L, p.max_level); l >= 0; --l) {
+        const size_t slot = (size_t)p.list_off[bi] + (size_t)l;
+        const int n = p.lst_n[slot];
+        const float* id = p.lst_d + slot * (size_t)p.efc;
+        const uint32_t* ii = p.lst_i + slot * (size_t)p.efc;
+        for (int j = lane; j < n; j += 64) {
+            w.list.d0[j] = id[j];
+            w.list.i0[j] = ii[j];
+        }
+        w.list.cur = 0;
+        w.list.size = n;
+        wave_sync();
+        const int m = l == 0 ? g.M0 : g.M;
+        const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, n, m, nsel_d);
+        uint32_t* row = g.row(node, l);
+        for (int j = lane; j < m; j += 64) row[j] = j < nsel ? w.sel[j] : VSG_EMPTY;
+        for (int j = lane; j < nsel; j += 64) {
+            const uint64_t key = ((uint64_t)l << PAIR_L_SHIFT) | ((uint64_t)w.sel[j] << PAIR_V_SHIFT) |
+                                 (uint64_t)node;
+            p.pair_keys[pos + j] = key;
+            p.pair_vals[pos + j] = __float_as_uint(w.seld[j]);
+        }
+        pos += (uint32_t)nsel;
+        wave_sync();
+    }
+    if (lane == 0 && p.stats) {
+        atomicAdd(&p.stats[3], (unsigned long long)nsel_d);
+        atomicAdd(&p.stats[5], (unsigned long long)nsel_d);
+    }
+}
+
 // ------------------------------------------------------------ build: rev --
 // Pairs sorted by (level, v, u).  Persistent waves scan contiguous chunks for
 // segment heads; each segment (level, v) is merged into v's row: append while
@@ -630,6 +732,26 @@ hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipSt
         if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3(p.nnodes), dim3(64), lds, s, p);
         err = hipGetLastError();
+    });
+    return err;
+}
+
+hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s) {
+    if (p.nnodes <= 0) return hipSuccess;
+    if (p.efc > 192 || !p.list_off || !p.lst_d || !p.lst_i || !p.lst_n) return hipErrorInvalidValue;
+    const size_t lds_beam = wave_lds_bytes(p.hash_size, p.efc, 0);
+    const size_t lds_sel = wave_lds_bytes(0, p.efc, sel_entries(p.g.M0));
+    hipError_t err = hipSuccess;
+    dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+        auto kb = VSG_KERNEL_OF(hnsw_insert_beam_kernel, sh, tt, mt);
+        auto ks = VSG_KERNEL_OF(hnsw_insert_select_kernel, sh, tt, mt);
+        if (lds_beam > 65536) (void)hipFuncSetAttribute((const void*)kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_beam);
+        hipLaunchKernelGGL(kb, dim3(p.nnodes), dim3(64), lds_beam, s, p);
+        err = hipGetLastError();
+        if (err == hipSuccess) {
+            hipLaunchKernelGGL(ks, dim3(p.nnodes), dim3(64), lds_sel, s, p);
+            err = hipGetLastError();
+        }
     });
     return err;
 }

@@ -240,7 +240,12 @@ struct vsg_index {
     int8_t* d_blevels = nullptr;
     uint32_t* d_pair_off = nullptr;
     uint32_t* d_bnodes = nullptr;
+    uint32_t* d_list_off = nullptr;  // split insert: first list slot of each batch node
     size_t bnodes_cap = 0;
+    float* d_lst_d = nullptr;  // split insert: per (node, level) sorted top-efc lists
+    uint32_t* d_lst_i = nullptr;
+    int* d_lst_n = nullptr;
+    size_t lst_cap = 0;  // lists
     uint64_t* d_pk[2] = {nullptr, nullptr};
     uint32_t* d_pv[2] = {nullptr, nullptr};
     size_t pairs_cap = 0;
@@ -319,6 +324,10 @@ static void free_dev(vsg_index* h) {
     hipFree(h->d_blevels);
     hipFree(h->d_pair_off);
     hipFree(h->d_bnodes);
+    hipFree(h->d_list_off);
+    hipFree(h->d_lst_d);
+    hipFree(h->d_lst_i);
+    hipFree(h->d_lst_n);
     for (int i = 0; i < 2; ++i) {
         hipFree(h->d_pk[i]);
         hipFree(h->d_pv[i]);
@@ -399,14 +408,34 @@ static int ensure_nodes(vsg_index* h, size_t n) {
     hipFree(h->d_blevels);
     hipFree(h->d_pair_off);
     hipFree(h->d_bnodes);
+    hipFree(h->d_list_off);
     h->d_blevels = nullptr;
     h->d_pair_off = nullptr;
     h->d_bnodes = nullptr;
+    h->d_list_off = nullptr;
     h->bnodes_cap = 0;
     HIP_TRY(dev_alloc(&h->d_blevels, want));
     HIP_TRY(dev_alloc(&h->d_pair_off, want));
     HIP_TRY(dev_alloc(&h->d_bnodes, want));
+    HIP_TRY(dev_alloc(&h->d_list_off, want));
     h->bnodes_cap = want;
+    return VSG_OK;
+}
+
+static int ensure_lists(vsg_index* h, size_t lists) {
+    if (lists <= h->lst_cap) return VSG_OK;
+    const size_t want = std::max(lists, h->lst_cap * 2);
+    hipFree(h->d_lst_d);
+    hipFree(h->d_lst_i);
+    hipFree(h->d_lst_n);
+    h->d_lst_d = nullptr;
+    h->d_lst_i = nullptr;
+    h->d_lst_n = nullptr;
+    h->lst_cap = 0;
+    HIP_TRY(dev_alloc(&h->d_lst_d, want * (size_t)h->efc));
+    HIP_TRY(dev_alloc(&h->d_lst_i, want * (size_t)h->efc));
+    HIP_TRY(dev_alloc(&h->d_lst_n, want));
+    h->lst_cap = want;
     return VSG_OK;
 }
 
@@ -730,6 +759,12 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     // at least 8 batches per call, so the call's own nodes find each other
     const size_t bcall = std::max<size_t>(1, n / 8);
     std::vector<uint32_t> pair_off(n);
+    // split insert (launch_insert_split): the efC beam at its own occupancy, then
+    // the selection; lists of (node, level) in HBM between the two (VSG_BUILD_SPLIT=0:
+    // the fused kernel; efC > 192 always fused)
+    const bool split = env_double("VSG_BUILD_SPLIT", 1) != 0 && h->efc <= 192;
+    std::vector<uint32_t> list_off(split ? n : 0);
+    size_t max_lists = 0;
     std::vector<Batch> plan;
     size_t max_pairs = 0;
     {
@@ -757,11 +792,16 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
                 }
             }
             // pair offsets: each node emits <= M0 + min(L, maxl) * M pairs
-            uint32_t acc = 0;
+            uint32_t acc = 0, lacc = 0;
             for (size_t j = 0; j < b; ++j) {
                 pair_off[i + j] = acc;
                 acc += (uint32_t)(h->M0 + std::min<int>(blev[i + j], maxl) * h->M);
+                if (split) {
+                    list_off[i + j] = lacc;
+                    lacc += (uint32_t)(std::min<int>(blev[i + j], maxl) + 1);
+                }
             }
+            max_lists = std::max<size_t>(max_lists, lacc);
             plan.push_back({i, b, (size_t)acc, entry, maxl, new_top, order[i + b - 1]});
             max_pairs = std::max<size_t>(max_pairs, acc);
             if (new_top >= 0) {
@@ -781,6 +821,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         for (const Batch& B : plan) max_b = std::max(max_b, B.b);
         if ((rc = ensure_locality(h, n, max_b, 0))) return rc;
     }
+    if (split && (rc = ensure_lists(h, max_lists))) return rc;
     if ((rc = ensure_pairs(h, max_pairs))) return rc;
     {
         size_t tmp = 0;
@@ -801,6 +842,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     HIP_TRY(hipMemcpyAsync(h->d_bnodes, order.data(), n * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_blevels, blev.data(), n, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_pair_off, pair_off.data(), n * 4, hipMemcpyHostToDevice, st));
+    if (split) HIP_TRY(hipMemcpyAsync(h->d_list_off, list_off.data(), n * 4, hipMemcpyHostToDevice, st));
     pc.mark("b:buffers+uploads");
 
     // pairs per reverse-kernel wave: with batches of up to 64k nodes, 64 pairs a
@@ -808,7 +850,10 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     // 0.075 s, C4 shard 1.32 -> 0.74 s (profiles/r02_build_schedule.jsonl)
     const size_t rgrid = (size_t)env_double("VSG_REVERSE_GRID", (double)h->reverse_grid);
     const size_t ppw = std::max<size_t>(1, (size_t)env_double("VSG_REVERSE_PAIRS_PER_WAVE", 64));
-    const int hash = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", 16));
+    // visited table of the insert beam: 16 x efC for rows >= 1 KiB, 8 x efC for
+    // shorter ones (a forgotten id costs one cheap re-read, a smaller table more
+    // resident beam waves: C4 shard insert -4 %, C2 no gain; profiles/r02_build_locality.jsonl)
+    const int hash = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", h->row_bytes >= 1024 ? 16 : 8));
     for (size_t bi = 0; bi < plan.size(); ++bi) {
         const Batch& B = plan[bi];
         hipEvent_t* ev = &h->ev_pool[4 * bi];
@@ -833,7 +878,15 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
             HIP_TRY(sort_pairs(h->d_sort_tmp, otmp, h->d_okey[0], h->d_okey[1], h->d_oidx[0], h->d_oidx[1], B.b, st));
             ip.perm = h->d_oidx[1];
         }
-        HIP_TRY(launch_insert(h->st, h->mk, ip, st));
+        if (split) {
+            ip.list_off = h->d_list_off + B.i;
+            ip.lst_d = h->d_lst_d;
+            ip.lst_i = h->d_lst_i;
+            ip.lst_n = h->d_lst_n;
+            HIP_TRY(launch_insert_split(h->st, h->mk, ip, st));
+        } else {
+            HIP_TRY(launch_insert(h->st, h->mk, ip, st));
+        }
         HIP_TRY(hipEventRecord(ev[1], st));
         size_t tmp = h->sort_tmp_bytes;
         HIP_TRY(sort_pairs(h->d_sort_tmp, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], B.npairs, st));

@@ -54,6 +54,14 @@ struct InsertParams {
     // Locality launch order (vsg_index.cpp build_slots): block b inserts batch
     // node perm[xcd_pos(b)] (nullptr: node b)
     const uint32_t* perm;
+    // Split insert (hnsw_insert_beam_kernel + hnsw_insert_select_kernel): the
+    // beam kernel stores each level's sorted top-efc list in HBM, the selection
+    // kernel reads it back.  List (node bi, level l) = slot list_off[bi] + l:
+    // lst_n[slot] entries at lst_d / lst_i[slot * efc ...].
+    const uint32_t* list_off;
+    float* lst_d;
+    uint32_t* lst_i;
+    int* lst_n;
 };
 
 struct ReverseParams {
@@ -143,6 +151,8 @@ size_t insert_lds_bytes(int efc, int hash, int m0);
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
 hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
 size_t search_reg_lds_bytes(int hash);
+// split insert: beam kernel then selection kernel (efc <= 192: register beam)
+hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s);
 hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s);
 hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s);
 hipError_t launch_exact(Storage st, MetricKind mk, const ExactParams& p, hipStream_t s);

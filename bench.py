@@ -347,8 +347,37 @@ def hnsw_leg(c, mode):
     }
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_workers(a):
+    """`--gpus N` with no launcher around us: start N ranks (one per GPU) under
+    torch.distributed.run as a CHILD process -- never an exec: nothing here has
+    touched the GPU yet, and the parent only waits -- and return its exit code.
+    Under a launcher (WORLD_SIZE set) the world size must equal --gpus, so a
+    run asked for N GPUs can never silently measure one."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {a.gpus}")
+        return None
+    if a.gpus <= 1:
+        return None
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     a = parse()
+    rc = launch_workers(a)
+    if rc is not None:
+        sys.exit(rc)
     c = Ctx(a)
     world, rank = c.world, c.rank
     if a.mode == "exact":

@@ -71,7 +71,7 @@ typedef struct {
     uint32_t dimensions;       /* Dimensions, src/lib.rs:146-147 */
     uint32_t metric;           /* VSG_METRIC_* */
     uint32_t quantization;     /* VSG_SCALAR_* storage in HBM (ScalarKind::F32, :95) */
-    uint32_t connectivity;     /* Connectivity (M), src/lib.rs:163-164; 0 => 16, max 32 */
+    uint32_t connectivity;     /* Connectivity (M), src/lib.rs:163-164; 0 => 16, 2..64 (level-0 rows of 2M) */
     uint32_t expansion_add;    /* ExpansionAdd (efC), src/lib.rs:181-182; 0 => 128 */
     uint32_t expansion_search; /* ExpansionSearch (ef), src/lib.rs:199-200; 0 => 64 */
     int32_t device;            /* HIP device ordinal (one shard per GPU) */
@@ -152,7 +152,11 @@ int vsg_index_set_upper_ef(vsg_index_t* index, size_t upper_ef);
 /* Device-resident variants: queries (f32 nq x dimensions), outputs and counts
  * (u32, optional) in device memory; enqueued on `stream` (NULL => the HIP
  * default stream) and NOT synchronised.  Used by bench.py and the multi-GPU
- * merge.  Concurrent add/remove must not overlap an enqueued search. */
+ * merge.  Writers may run beside an enqueued search: each one records a
+ * completion event, and a writer that frees or rewrites memory the search may
+ * read (capacity growth, compaction, the f16 copy's reallocation) first waits
+ * for every such event; appends and removes do not wait (the search sees a
+ * prefix of them, as with vsg_index_search). */
 int vsg_index_search_device(vsg_index_t* index, const float* queries_device, size_t nq, size_t k,
                             size_t ef, uint64_t* out_keys_device, float* out_distances_device,
                             uint32_t* out_counts_device, void* stream);
@@ -221,6 +225,70 @@ int vsg_index_file_info(const char* path, vsg_file_info_t* out);
 int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed,
                        size_t start_row, float* out_device, void* stream);
 
+/* ---------------------------------------------------------- Sharded index --
+ * One logical index row-sharded over the GPUs of a node (SURVEY §8b
+ * `create(opts{..., n_gpus, seed})`, §8e; north_star: "the index shards by
+ * row-range across the 8 GPUs of one node with per-shard top-k merged over
+ * xGMI").  Shard g is a vsg_index_t on devices[g] with its own HNSW graph;
+ * several shards may share a device.  A key lives on shard vsg_sharded_route()
+ * = splitmix64(key) mod n_shards: balanced for any key stream (the reference
+ * allocates monotonic keys, usearch.rs:181), and a duplicate or replaced key
+ * always meets its live copy on the same shard.
+ *   add     splits the batch by shard, checks every shard for reserved and
+ *           duplicate keys first (any => nothing is inserted, as
+ *           vsg_index_add), then builds all shards concurrently: one host
+ *           thread and stream per shard, no communication.
+ *   search  broadcasts the queries to each shard device, searches every shard
+ *           concurrently (top-k per shard), gathers the per-shard rows to the
+ *           answering device (peer DMA over xGMI; a device-local copy when a
+ *           shard lives there) and k-way merges them (merge_topk64_kernel):
+ *           rows ascending by (distance, key), padded with VSG_NO_KEY / +inf.
+ * Replaces the one-device usearch::Index of src/index/usearch.rs:89-99 when an
+ * index is spread over several GPUs.  Thread-safety as vsg_index_t; writers
+ * serialise on the sharded index. */
+typedef struct vsg_sharded vsg_sharded_t;
+
+#define VSG_MAX_SHARDS 64
+
+typedef struct {
+    vsg_index_options_t index; /* every shard's options; index.device is ignored, shard g's
+                                  level seed is index.seed + g */
+    uint32_t n_shards;         /* 1 .. VSG_MAX_SHARDS */
+    int32_t answer_device;     /* device that merges and returns results; -1 => devices[0] */
+    const int32_t* devices;    /* n_shards device ordinals (repeats allowed); NULL => shard g
+                                  on device g mod (visible device count) */
+} vsg_sharded_options_t;
+
+int vsg_sharded_new(const vsg_sharded_options_t* options, vsg_sharded_t** out);
+void vsg_sharded_free(vsg_sharded_t* index);
+/* each shard reserves ceil(capacity / n_shards) (shards also grow on add) */
+int vsg_sharded_reserve(vsg_sharded_t* index, size_t capacity);
+size_t vsg_sharded_capacity(const vsg_sharded_t* index); /* sum over shards */
+size_t vsg_sharded_size(const vsg_sharded_t* index);     /* live rows, sum over shards */
+size_t vsg_sharded_dimensions(const vsg_sharded_t* index);
+int vsg_sharded_contains(const vsg_sharded_t* index, uint64_t key);
+size_t vsg_sharded_shard_count(const vsg_sharded_t* index);
+uint32_t vsg_sharded_route(const vsg_sharded_t* index, uint64_t key);
+/* borrowed handle of shard g (stats, export, save); valid until vsg_sharded_free */
+vsg_index_t* vsg_sharded_shard(vsg_sharded_t* index, size_t g);
+int vsg_sharded_add(vsg_sharded_t* index, const uint64_t* keys, const float* vectors, size_t n);
+int vsg_sharded_remove(vsg_sharded_t* index, const uint64_t* keys, size_t n, size_t* n_removed);
+/* as vsg_index_search / _exact_search: every shard returns its top k */
+int vsg_sharded_search(vsg_sharded_t* index, const float* queries, size_t nq, size_t k, size_t ef,
+                       uint64_t* out_keys, float* out_distances, size_t* out_counts);
+int vsg_sharded_exact_search(vsg_sharded_t* index, const float* queries, size_t nq, size_t k,
+                             uint64_t* out_keys, float* out_distances, size_t* out_counts);
+/* Device-resident: queries and outputs on the answering device, enqueued on
+ * `stream` (a stream of that device) and not synchronised.  exact != 0 =>
+ * brute force. */
+int vsg_sharded_search_device(vsg_sharded_t* index, const float* queries_device, size_t nq, size_t k,
+                              size_t ef, int exact, uint64_t* out_keys_device,
+                              float* out_distances_device, void* stream);
+int vsg_sharded_compact(vsg_sharded_t* index, size_t* n_dropped);
+/* counters summed over shards (device times: the sum of every shard's) */
+int vsg_sharded_stats(const vsg_sharded_t* index, vsg_stats_t* out);
+int vsg_sharded_reset_stats(vsg_sharded_t* index);
+
 /* ------------------------------------------------------------------ Actor --
  * The reference's per-index actor (src/index/usearch.rs:82-311: an mpsc
  * channel of Index::{AddOrReplace, Remove, Ann, Count} messages served by
@@ -258,12 +326,23 @@ typedef struct {
 
 /* replaces usearch::new (the actor spawn + Index::new + reserve(1M)) — usearch.rs:82-139 */
 int vsg_actor_new(const vsg_actor_options_t* options, vsg_actor_t** out);
+/* Same actor over a sharded index: options->index is every shard's options,
+ * shard g on devices[g] (NULL => g mod device count), results merged on devices[0]. */
+int vsg_actor_new_sharded(const vsg_actor_options_t* options, uint32_t n_shards, const int32_t* devices,
+                          vsg_actor_t** out);
 /* drains queued messages, stops the worker, frees the index (channel close, :129) */
 void vsg_actor_free(vsg_actor_t* actor);
 /* Index::AddOrReplace — usearch.rs:174-233.  Asynchronous (the reference's
  * channel send); failures inside the worker are counted (add_errors), as the
  * reference logs and swallows them (:207-224). */
 int vsg_actor_add_or_replace(vsg_actor_t* actor, uint64_t key, const float* embedding, size_t dims);
+/* Same, with a completion: `done(ctx, key, status)` runs on the actor's worker
+ * thread once the batched add carrying this message finished (status VSG_OK or
+ * the add's error).  The reference awaits every add and drops the new PK<->key
+ * mapping when it failed (usearch.rs:198-232); the host shim does that here. */
+typedef void (*vsg_add_done_fn)(void* ctx, uint64_t key, int status);
+int vsg_actor_add_or_replace_cb(vsg_actor_t* actor, uint64_t key, const float* embedding, size_t dims,
+                                vsg_add_done_fn done, void* ctx);
 /* Index::Remove — usearch.rs:235-249 (asynchronous; unknown keys are ignored) */
 int vsg_actor_remove(vsg_actor_t* actor, uint64_t key);
 /* Index::Ann — usearch.rs:251-306.  Blocks until answered.  Dimension errors
@@ -273,12 +352,18 @@ int vsg_actor_ann(vsg_actor_t* actor, const float* embedding, size_t dims, size_
                   uint64_t* out_keys, float* out_distances, size_t* out_count);
 /* Index::Count — usearch.rs:308-311 (live size) */
 int vsg_actor_count(vsg_actor_t* actor, size_t* out);
+/* Index::Count as the reference computes it (usearch.rs:308-311: a read-lock
+ * size() beside fire-and-forget adds): the live size now, without queueing
+ * behind pending writes (vsg_actor_count waits for them in submission order) */
+size_t vsg_actor_size(const vsg_actor_t* actor);
 /* wait until all previously submitted writes (and, in submission-order mode,
  * every other message) are applied */
 int vsg_actor_flush(vsg_actor_t* actor);
 int vsg_actor_counters(const vsg_actor_t* actor, vsg_actor_counters_t* out);
-/* borrowed handle of the actor's index (stats, export); valid until vsg_actor_free */
+/* borrowed handle of the actor's index (stats, export); valid until vsg_actor_free.
+ * A sharded actor returns its shard 0 here and the whole index from vsg_actor_sharded. */
 vsg_index_t* vsg_actor_index(vsg_actor_t* actor);
+vsg_sharded_t* vsg_actor_sharded(vsg_actor_t* actor); /* NULL for a one-device actor */
 
 /* splitmix64 level draw; bit-identical to oracle/vsg_oracle.c */
 int vsg_sample_level(uint64_t seed, uint64_t slot, uint32_t connectivity);

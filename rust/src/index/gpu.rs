@@ -15,9 +15,19 @@
 //! key takes the next one, nothing is rolled back (the reference's `fetch_sub`
 //! rollback at :191 can hand one key to two primary keys).
 //!
+//! A failed add drops its PK <-> key mapping again, as usearch.rs:230-232 does: the add
+//! goes through vsg_actor_add_or_replace_cb, whose completion runs `add_done` on the native
+//! worker thread.  Count is the reference's read-lock size() (usearch.rs:308-311):
+//! vsg_actor_size, which does not queue behind pending writes.
+//!
+//! One index may span several GPUs: `new_gpu_sharded(devices)` creates every index as a
+//! row-sharded vsg_sharded_t (one HNSW shard per entry of `devices`, keys routed by hash,
+//! per-shard top-k merged on devices[0] over xGMI; include/vsg.h "Sharded index").
+//!
 //! Symbol sequence a lifecycle drives (mirrored by tests/cpp/test_rust_call_sequence.cpp):
-//!   vsg_actor_new (vsg_index_new + reserve(1M)) -> vsg_actor_add_or_replace* ->
-//!   vsg_actor_remove -> vsg_actor_ann -> vsg_actor_count -> vsg_actor_free.
+//!   vsg_actor_new | vsg_actor_new_sharded (index(es) + reserve(1M)) ->
+//!   vsg_actor_add_or_replace_cb* -> vsg_actor_remove -> vsg_actor_ann -> vsg_actor_size ->
+//!   vsg_actor_free.
 
 use crate::Connectivity;
 use crate::Dimensions;
@@ -36,6 +46,7 @@ use anyhow::anyhow;
 use bimap::BiMap;
 use std::ffi::CStr;
 use std::os::raw::c_int;
+use std::os::raw::c_void;
 use std::sync::Arc;
 use std::sync::RwLock;
 use tokio::sync::mpsc;
@@ -55,30 +66,52 @@ fn check(rc: c_int) -> anyhow::Result<()> {
 }
 
 /// Owned native actor.  Every vsg_actor_* entry point is thread-safe (vsg.h).
-struct GpuActor(*mut sys::vsg_actor_t);
+/// `keys` is the context of the add completions: declared after `ptr`, it outlives
+/// the actor's drain in `drop` (fields drop after `Drop::drop` returns).
+struct GpuActor {
+    ptr: *mut sys::vsg_actor_t,
+    keys: Keys,
+}
 unsafe impl Send for GpuActor {}
 unsafe impl Sync for GpuActor {}
 
 impl Drop for GpuActor {
     fn drop(&mut self) {
-        // drains queued messages, joins the worker, frees the HBM index
-        unsafe { sys::vsg_actor_free(self.0) }
+        // drains queued messages (running their completions), joins the worker, frees HBM
+        unsafe { sys::vsg_actor_free(self.ptr) }
     }
 }
 
+/// Completion of one add (worker thread): a failed add forgets its mapping, usearch.rs:230-232.
+unsafe extern "C" fn add_done(ctx: *mut c_void, key: u64, status: c_int) {
+    if status == sys::VSG_OK {
+        return;
+    }
+    debug!("add_or_replace: unable to add embedding for key {key}: vsg error {status}");
+    let keys = unsafe { &*(ctx as *const RwLock<KeyMap>) };
+    keys.write().unwrap().map.remove_by_right(&key);
+}
+
 impl GpuActor {
-    fn new(options: &sys::vsg_actor_options_t) -> anyhow::Result<Self> {
+    fn new(options: &sys::vsg_actor_options_t, devices: &[i32], keys: Keys) -> anyhow::Result<Self> {
         let mut a = std::ptr::null_mut();
-        check(unsafe { sys::vsg_actor_new(options, &mut a) })?;
-        Ok(Self(a))
+        if devices.len() > 1 {
+            check(unsafe { sys::vsg_actor_new_sharded(options, devices.len() as u32, devices.as_ptr(), &mut a) })?;
+        } else {
+            check(unsafe { sys::vsg_actor_new(options, &mut a) })?;
+        }
+        Ok(Self { ptr: a, keys })
     }
 
     fn add_or_replace(&self, key: u64, embedding: &[f32]) -> anyhow::Result<()> {
-        check(unsafe { sys::vsg_actor_add_or_replace(self.0, key, embedding.as_ptr(), embedding.len()) })
+        let ctx = Arc::as_ptr(&self.keys) as *mut c_void;
+        check(unsafe {
+            sys::vsg_actor_add_or_replace_cb(self.ptr, key, embedding.as_ptr(), embedding.len(), Some(add_done), ctx)
+        })
     }
 
     fn remove(&self, key: u64) -> anyhow::Result<()> {
-        check(unsafe { sys::vsg_actor_remove(self.0, key) })
+        check(unsafe { sys::vsg_actor_remove(self.ptr, key) })
     }
 
     /// Blocks until the batched search holding this query returns.
@@ -87,7 +120,7 @@ impl GpuActor {
         let mut distances = vec![f32::INFINITY; limit];
         let mut n = 0usize;
         check(unsafe {
-            sys::vsg_actor_ann(self.0, embedding.as_ptr(), embedding.len(), limit, keys.as_mut_ptr(),
+            sys::vsg_actor_ann(self.ptr, embedding.as_ptr(), embedding.len(), limit, keys.as_mut_ptr(),
                                distances.as_mut_ptr(), &mut n)
         })?;
         keys.truncate(n);
@@ -95,19 +128,17 @@ impl GpuActor {
         Ok((keys, distances))
     }
 
-    fn count(&self) -> anyhow::Result<usize> {
-        let mut n = 0usize;
-        check(unsafe { sys::vsg_actor_count(self.0, &mut n) })?;
-        Ok(n)
+    /// live size now, under the index's shared lock (does not wait for queued writes)
+    fn size(&self) -> usize {
+        unsafe { sys::vsg_actor_size(self.ptr) }
     }
 }
 
 /// `IndexFactory` for GPU-backed vector indexes (replaces `UsearchIndexFactory`,
-/// usearch.rs:36-58).  One factory per GPU: every index it creates lives in that
-/// GPU's HBM (row-range sharding over the node's GPUs is the Python/RCCL layer's job,
-/// vsg/distributed.py).
+/// usearch.rs:36-58).  Every index it creates lives on `devices`: one GPU's HBM, or one
+/// row shard per listed GPU (vsg_sharded_t, merged on devices[0]).
 pub struct GpuIndexFactory {
-    device: i32,
+    devices: Vec<i32>,
     metric: u32,
 }
 
@@ -120,21 +151,30 @@ impl IndexFactory for GpuIndexFactory {
         expansion_add: ExpansionAdd,
         expansion_search: ExpansionSearch,
     ) -> anyhow::Result<mpsc::Sender<Index>> {
-        new(id, dimensions, connectivity, expansion_add, expansion_search, self.device, self.metric)
+        new(id, dimensions, connectivity, expansion_add, expansion_search, &self.devices, self.metric)
     }
 }
 
 /// GPU `device`, cosine metric.  usearch left the metric to its crate default
 /// (usearch.rs:89-96); here it is explicit.
 pub fn new_gpu(device: i32) -> anyhow::Result<GpuIndexFactory> {
-    Ok(GpuIndexFactory { device, metric: sys::VSG_METRIC_COS })
+    Ok(GpuIndexFactory { devices: vec![device], metric: sys::VSG_METRIC_COS })
 }
 
 pub fn new_gpu_with_metric(device: i32, metric: u32) -> anyhow::Result<GpuIndexFactory> {
     if metric > sys::VSG_METRIC_COS {
         return Err(anyhow!("unknown metric {metric}"));
     }
-    Ok(GpuIndexFactory { device, metric })
+    Ok(GpuIndexFactory { devices: vec![device], metric })
+}
+
+/// Every index row-sharded over `devices` (e.g. the node's 8 GPUs: `&[0, 1, .., 7]`),
+/// cosine metric; results are merged on `devices[0]`.
+pub fn new_gpu_sharded(devices: &[i32]) -> anyhow::Result<GpuIndexFactory> {
+    if devices.is_empty() || devices.len() > sys::VSG_MAX_SHARDS as usize {
+        return Err(anyhow!("between 1 and {} shard devices", sys::VSG_MAX_SHARDS));
+    }
+    Ok(GpuIndexFactory { devices: devices.to_vec(), metric: sys::VSG_METRIC_COS })
 }
 
 const CHANNEL_SIZE: usize = 10; // as usearch.rs:102
@@ -153,7 +193,7 @@ pub(crate) fn new(
     connectivity: Connectivity,
     expansion_add: ExpansionAdd,
     expansion_search: ExpansionSearch,
-    device: i32,
+    devices: &[i32],
     metric: u32,
 ) -> anyhow::Result<mpsc::Sender<Index>> {
     let options = sys::vsg_actor_options_t {
@@ -164,7 +204,7 @@ pub(crate) fn new(
             connectivity: connectivity.0 as u32, // 0 => usearch defaults (src/db.rs:400-410)
             expansion_add: expansion_add.0 as u32,
             expansion_search: expansion_search.0 as u32,
-            device,
+            device: devices[0],
             flags: 0,
             seed: 0,
         },
@@ -175,12 +215,12 @@ pub(crate) fn new(
         concurrent_reads: 1,
         ..Default::default()
     };
-    let actor = Arc::new(GpuActor::new(&options)?);
+    let keys: Keys = Arc::new(RwLock::new(KeyMap { map: BiMap::new(), next: 0 }));
+    let actor = Arc::new(GpuActor::new(&options, devices, Arc::clone(&keys))?);
     let (tx, mut rx) = mpsc::channel(CHANNEL_SIZE);
     tokio::spawn(
         async move {
             debug!("starting");
-            let keys: Keys = Arc::new(RwLock::new(KeyMap { map: BiMap::new(), next: 0 }));
             while let Some(msg) = rx.recv().await {
                 process(msg, dimensions, Arc::clone(&actor), Arc::clone(&keys)).await;
             }
@@ -219,8 +259,10 @@ fn add_or_replace(actor: &GpuActor, keys: &Keys, primary_key: PrimaryKey, embedd
             }
         }
     };
+    // a failure inside the batched add arrives in `add_done`; a rejected message here
     if let Err(err) = actor.add_or_replace(key, &embedding.0) {
         debug!("add_or_replace: unable to add embedding for key {key}: {err}");
+        keys.write().unwrap().map.remove_by_right(&key); // usearch.rs:230-232
     }
 }
 
@@ -257,7 +299,7 @@ fn ann(actor: &GpuActor, keys: &Keys, tx: oneshot::Sender<AnnR>, embedding: Embe
     tx.send(result).unwrap_or_else(|_| trace!("ann: unable to send response"));
 }
 
-/// usearch.rs:308-311 (live size)
+/// usearch.rs:308-311: the live size under a read lock, answered at once
 fn count(actor: &GpuActor, tx: oneshot::Sender<CountR>) {
-    tx.send(actor.count()).unwrap_or_else(|_| trace!("count: unable to send response"));
+    tx.send(Ok(actor.size())).unwrap_or_else(|_| trace!("count: unable to send response"));
 }

@@ -108,6 +108,26 @@ pub struct vsg_actor_counters_t {
 }
 
 #[repr(C)]
+pub struct vsg_sharded_t {
+    _opaque: [u8; 0],
+}
+
+pub const VSG_MAX_SHARDS: u32 = 64;
+
+/// One logical index row-sharded over the node's GPUs (SURVEY §8b `n_gpus`).
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct vsg_sharded_options_t {
+    pub index: vsg_index_options_t, // every shard's options (device ignored, seed + g per shard)
+    pub n_shards: u32,              // 1 ..= VSG_MAX_SHARDS
+    pub answer_device: i32,         // -1 => devices[0]
+    pub devices: *const i32,        // n_shards ordinals (repeats allowed); null => g % device count
+}
+
+/// Completion of one AddOrReplace (vsg_actor_add_or_replace_cb), on the actor's worker thread.
+pub type vsg_add_done_fn = Option<unsafe extern "C" fn(ctx: *mut c_void, key: u64, status: c_int)>;
+
+#[repr(C)]
 #[derive(Clone, Copy, Debug, Default)]
 pub struct vsg_file_info_t {
     pub options: vsg_index_options_t,
@@ -166,10 +186,39 @@ extern "C" {
     pub fn vsg_datagen_device(kind: c_int, n: usize, dim: usize, seed: u64, model_seed: u64, start_row: usize,
                               out_device: *mut f32, stream: *mut c_void) -> c_int;
 
+    // one index row-sharded over several GPUs
+    pub fn vsg_sharded_new(options: *const vsg_sharded_options_t, out: *mut *mut vsg_sharded_t) -> c_int;
+    pub fn vsg_sharded_free(index: *mut vsg_sharded_t);
+    pub fn vsg_sharded_reserve(index: *mut vsg_sharded_t, capacity: usize) -> c_int;
+    pub fn vsg_sharded_capacity(index: *const vsg_sharded_t) -> usize;
+    pub fn vsg_sharded_size(index: *const vsg_sharded_t) -> usize;
+    pub fn vsg_sharded_dimensions(index: *const vsg_sharded_t) -> usize;
+    pub fn vsg_sharded_contains(index: *const vsg_sharded_t, key: u64) -> c_int;
+    pub fn vsg_sharded_shard_count(index: *const vsg_sharded_t) -> usize;
+    pub fn vsg_sharded_route(index: *const vsg_sharded_t, key: u64) -> u32;
+    pub fn vsg_sharded_shard(index: *mut vsg_sharded_t, g: usize) -> *mut vsg_index_t;
+    pub fn vsg_sharded_add(index: *mut vsg_sharded_t, keys: *const u64, vectors: *const f32, n: usize) -> c_int;
+    pub fn vsg_sharded_remove(index: *mut vsg_sharded_t, keys: *const u64, n: usize, n_removed: *mut usize) -> c_int;
+    pub fn vsg_sharded_search(index: *mut vsg_sharded_t, queries: *const f32, nq: usize, k: usize, ef: usize,
+                              out_keys: *mut u64, out_distances: *mut f32, out_counts: *mut usize) -> c_int;
+    pub fn vsg_sharded_exact_search(index: *mut vsg_sharded_t, queries: *const f32, nq: usize, k: usize,
+                                    out_keys: *mut u64, out_distances: *mut f32, out_counts: *mut usize) -> c_int;
+    pub fn vsg_sharded_search_device(index: *mut vsg_sharded_t, queries_device: *const f32, nq: usize, k: usize,
+                                     ef: usize, exact: c_int, out_keys_device: *mut u64,
+                                     out_distances_device: *mut f32, stream: *mut c_void) -> c_int;
+    pub fn vsg_sharded_compact(index: *mut vsg_sharded_t, n_dropped: *mut usize) -> c_int;
+    pub fn vsg_sharded_stats(index: *const vsg_sharded_t, out: *mut vsg_stats_t) -> c_int;
+    pub fn vsg_sharded_reset_stats(index: *mut vsg_sharded_t) -> c_int;
+
     // the per-index actor (usearch.rs:82-311) with request coalescing
     pub fn vsg_actor_new(options: *const vsg_actor_options_t, out: *mut *mut vsg_actor_t) -> c_int;
     pub fn vsg_actor_free(actor: *mut vsg_actor_t);
+    pub fn vsg_actor_new_sharded(options: *const vsg_actor_options_t, n_shards: u32, devices: *const i32,
+                                 out: *mut *mut vsg_actor_t) -> c_int;
     pub fn vsg_actor_add_or_replace(actor: *mut vsg_actor_t, key: u64, embedding: *const f32, dims: usize) -> c_int;
+    pub fn vsg_actor_add_or_replace_cb(actor: *mut vsg_actor_t, key: u64, embedding: *const f32, dims: usize,
+                                       done: vsg_add_done_fn, ctx: *mut c_void) -> c_int;
+    pub fn vsg_actor_size(actor: *const vsg_actor_t) -> usize;
     pub fn vsg_actor_remove(actor: *mut vsg_actor_t, key: u64) -> c_int;
     pub fn vsg_actor_ann(actor: *mut vsg_actor_t, embedding: *const f32, dims: usize, limit: usize,
                          out_keys: *mut u64, out_distances: *mut f32, out_count: *mut usize) -> c_int;
@@ -177,6 +226,7 @@ extern "C" {
     pub fn vsg_actor_flush(actor: *mut vsg_actor_t) -> c_int;
     pub fn vsg_actor_counters(actor: *const vsg_actor_t, out: *mut vsg_actor_counters_t) -> c_int;
     pub fn vsg_actor_index(actor: *mut vsg_actor_t) -> *mut vsg_index_t;
+    pub fn vsg_actor_sharded(actor: *mut vsg_actor_t) -> *mut vsg_sharded_t;
 
     pub fn vsg_sample_level(seed: u64, slot: u64, connectivity: u32) -> c_int;
     pub fn vsg_last_error() -> *const c_char;

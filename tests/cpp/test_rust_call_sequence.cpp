@@ -9,8 +9,13 @@
 //  2. the actor path gpu.rs uses (vsg_actor_*, concurrent_reads = 1): the reference's own
 //     unit KAT (usearch.rs:322-425, D = 3, keys 1/2/3, replace, remove, count) with its
 //     polling (anns may run before earlier writes land, as the reference's fire-and-forget
-//     adds allow; it polls for 10 s, usearch.rs:352-358).
+//     adds allow; it polls for 10 s, usearch.rs:352-358).  Adds go through
+//     vsg_actor_add_or_replace_cb (gpu.rs rolls the BiMap back from the completion,
+//     usearch.rs:230-232), counts through vsg_actor_size (usearch.rs:308-311).  Run once
+//     on a one-device actor (new_gpu) and once on a two-shard actor on device 0
+//     (new_gpu_sharded(&[0, 0]), vsg_actor_new_sharded).
 // Metric l2sq: the KAT is an f32 rounding tie under cosine.
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -70,18 +75,24 @@ static bool ann_becomes(vsg_actor_t* a, const float* q, uint64_t want) {
     return false;
 }
 
+// count as gpu.rs answers Index::Count (vsg_actor_size), polled like the reference test
 static bool count_becomes(vsg_actor_t* a, size_t want) {
     const auto t0 = std::chrono::steady_clock::now();
     while (std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10)) {
-        size_t n = 0;
-        if (vsg_actor_count(a, &n) != VSG_OK) return false;
-        if (n == want) return true;
+        if (vsg_actor_size(a) == want) return true;
         std::this_thread::sleep_for(std::chrono::milliseconds(1));
     }
     return false;
 }
 
-static void actor_kat() {
+// gpu.rs add_done: counts completions; a failure would drop the BiMap entry
+static std::atomic<int> g_done{0}, g_failed{0};
+static void add_done(void*, uint64_t, int status) {
+    g_done++;
+    if (status != VSG_OK) g_failed++;
+}
+
+static void actor_kat(bool sharded) {
     vsg_actor_options_t o{};
     o.index.dimensions = 3;
     o.index.metric = VSG_METRIC_L2SQ;
@@ -89,17 +100,26 @@ static void actor_kat() {
     o.reserve_threshold = 1000000 / 3;
     o.concurrent_reads = 1;  // as rust/src/index/gpu.rs
     vsg_actor_t* a = nullptr;
-    CHECK(vsg_actor_new(&o, &a) == VSG_OK);
+    const int32_t devs[2] = {0, 0};
+    if (sharded) {
+        CHECK(vsg_actor_new_sharded(&o, 2, devs, &a) == VSG_OK);
+        CHECK(vsg_actor_sharded(a) != nullptr && vsg_sharded_shard_count(vsg_actor_sharded(a)) == 2);
+    } else {
+        CHECK(vsg_actor_new(&o, &a) == VSG_OK);
+        CHECK(vsg_actor_sharded(a) == nullptr);
+    }
+    g_done = 0;
+    g_failed = 0;
     // PrimaryKey -> u64 as gpu.rs allocates them: 1 -> 0, 2 -> 1, 3 -> 2
     const float r1[3] = {1, 1, 1}, r2[3] = {2, -2, 2}, r3[3] = {3, 3, 3};
-    CHECK(vsg_actor_add_or_replace(a, 0, r1, 3) == VSG_OK);
-    CHECK(vsg_actor_add_or_replace(a, 1, r2, 3) == VSG_OK);
-    CHECK(vsg_actor_add_or_replace(a, 2, r3, 3) == VSG_OK);
+    CHECK(vsg_actor_add_or_replace_cb(a, 0, r1, 3, add_done, nullptr) == VSG_OK);
+    CHECK(vsg_actor_add_or_replace_cb(a, 1, r2, 3, add_done, nullptr) == VSG_OK);
+    CHECK(vsg_actor_add_or_replace_cb(a, 2, r3, 3, add_done, nullptr) == VSG_OK);
     CHECK(count_becomes(a, 3));
     const float q[3] = {2.2f, -2.2f, 2.2f};
     CHECK(ann_becomes(a, q, 1));  // PK 2
     const float r3b[3] = {2.1f, -2.1f, 2.1f};
-    CHECK(vsg_actor_add_or_replace(a, 2, r3b, 3) == VSG_OK);  // replace PK 3: same key
+    CHECK(vsg_actor_add_or_replace_cb(a, 2, r3b, 3, add_done, nullptr) == VSG_OK);  // replace PK 3: same key
     CHECK(ann_becomes(a, q, 2));  // PK 3
     CHECK(vsg_actor_remove(a, 2) == VSG_OK);
     CHECK(count_becomes(a, 2));
@@ -113,13 +133,21 @@ static void actor_kat() {
     CHECK(vsg_actor_flush(a) == VSG_OK);
     vsg_actor_counters_t c{};
     CHECK(vsg_actor_counters(a, &c) == VSG_OK && c.add_errors == 0);
-    CHECK(vsg_actor_index(a) != nullptr && vsg_index_size(vsg_actor_index(a)) == 2);
+    CHECK(g_done == 4 && g_failed == 0);
+    if (sharded) {
+        CHECK(vsg_sharded_size(vsg_actor_sharded(a)) == 2);
+    } else {
+        CHECK(vsg_actor_index(a) != nullptr && vsg_index_size(vsg_actor_index(a)) == 2);
+    }
+    // a rejected message: wrong dimensions (gpu.rs drops the new mapping at once)
+    CHECK(vsg_actor_add_or_replace_cb(a, 7, r1, 2, add_done, nullptr) == VSG_EINVAL);
     vsg_actor_free(a);
 }
 
 int main() {
     direct_index();
-    actor_kat();
+    actor_kat(false);
+    actor_kat(true);
     std::printf("ok\n");
     return 0;
 }

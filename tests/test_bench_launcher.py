@@ -1,0 +1,40 @@
+"""bench.py --gpus N (VERDICT r2 missing #3): with no launcher around it, bench.py starts N
+ranks under torch.distributed.run as a child process; under a launcher, WORLD_SIZE must
+equal --gpus, so a run asked for N GPUs can never silently measure one."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def test_world_size_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "1"], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode != 0
+    assert "WORLD_SIZE=2 but --gpus 1" in out.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gpus_2_launches_two_ranks():
+    """Two gloo ranks rehearsed on the one GPU of the box: the JSON line reports n_gpus 2
+    and the row-shard leg (every query on both shards, all-gather + merge)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "2", "--dist-backend", "gloo",
+                          "--rows", "100000", "--queries", "2000", "--gt-queries", "2000", "--steps", "2",
+                          "--warmup", "1", "--config-ef", "0", "--upper-ef", "0", "--rerank-leg", "0", "--no-cpu"],
+                         env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [json.loads(s) for s in out.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = lines[0]
+    assert r["n_gpus"] == 2
+    assert r["config"]["parallelism"].startswith("row-shard x2")
+    assert r["config"]["recall_at_10"] >= 0.95
+    assert r["replica_mode"]["queries_per_step"] == 4000

@@ -136,7 +136,7 @@ def test_load_validates_crafted_graph(tmp_path):
     ids past the slot count, an entry point off the top level, upper rows outside
     the table, a reserved live key -- each refused before any kernel reads it."""
     from test_persistence_format import write_file
-    M, slots = 4, 6
+    M, slots, E = 4, 6, 0xFFFFFFFF
     chain = np.full((slots, 2 * M), 0xFFFFFFFF, np.uint32)
     for s in range(slots):  # a ring on level 0
         chain[s, 0], chain[s, 1] = (s + 1) % slots, (s - 1) % slots
@@ -145,6 +145,11 @@ def test_load_validates_crafted_graph(tmp_path):
     write_file(p, **ok)
     b = vsg.Index.load(p)
     assert b.size() == slots and int(b.search(np.zeros((1, 8), np.float32), 3).counts[0]) == 3
+    # a valid two-level graph still loads: slot 2 (level 1, the entry) links slot 4 (level 1)
+    two = dict(ok, levels=[0, 0, 1, 0, 1, 0], max_level=1, upper_rows=2, upper_off=[E, E, 0, E, 1, E],
+               upper=[4, E, E, E, 2, E, E, E])
+    write_file(p, **two)
+    assert int(vsg.Index.load(p).search(np.zeros((1, 8), np.float32), 3).counts[0]) == 3
     bad = chain.copy()
     bad[3, 2] = slots + 5
     cases = [(dict(ok, adj0=bad), "adjacency"),
@@ -153,6 +158,9 @@ def test_load_validates_crafted_graph(tmp_path):
              (dict(ok, levels=[0, 0, 0, 1, 0, 0]), "level"),
              (dict(ok, levels=[0, 0, 1, 0, 0, 0], max_level=1, upper_off=[0xFFFFFFFF, 0xFFFFFFFF, 0] + [0xFFFFFFFF] * 3),
               "upper rows"),
+             # an upper row of level 1 naming a level-0 node (its upper_off is EMPTY)
+             (dict(ok, levels=[0, 0, 1, 0, 0, 0], max_level=1, upper_rows=1, upper_off=[E, E, 0, E, E, E],
+                   upper=[4, E, E, E]), "below that level"),
              (dict(ok, keys=[0, 1, 2, 2**64 - 2, 4, 5]), "reserved"),
              (dict(ok, keys=[0, 1, 2, 3, 3, 5]), "duplicate")]
     for kw, msg in cases:
@@ -176,6 +184,14 @@ def test_import_validates_graph():
     with pytest.raises(vsg.VsgError, match="entry"):
         h.import_graph(g)
     g["entry"] = 0
+    # slot 0 (level 1, the entry) lists slot 5 (level 0) in its level-1 row
+    g2 = dict(g, levels=np.zeros(n, np.int8), max_level=1, upper=np.full((1, 4), 0xFFFFFFFF, np.uint32),
+              upper_off=np.full(n, 0xFFFFFFFF, np.uint32))
+    g2["levels"][0] = 1
+    g2["upper_off"][0] = 0
+    g2["upper"][0, 0] = 5
+    with pytest.raises(vsg.VsgError, match="below that level"):
+        h.import_graph(g2)
     h.import_graph(g)
     assert h.size() == n
 

@@ -45,7 +45,8 @@ def test_rust_ffi_declares_every_header_symbol_and_all_are_exported():
 @pytest.mark.parametrize("rust,ctype", [("vsg_index_options_t", _lib.Options), ("vsg_stats_t", _lib.Stats),
                                         ("vsg_actor_options_t", _lib.ActorOptions),
                                         ("vsg_actor_counters_t", _lib.ActorCounters),
-                                        ("vsg_file_info_t", _lib.FileInfo)])
+                                        ("vsg_file_info_t", _lib.FileInfo),
+                                        ("vsg_sharded_options_t", _lib.ShardedOptions)])
 def test_rust_struct_layouts_match_header(rust, ctype):
     assert _rust_struct_fields(rust) == [f for f, _ in ctype._fields_]
 

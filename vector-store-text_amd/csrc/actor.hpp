@@ -112,12 +112,18 @@ class Actor {
         }
     };
 
+    // completion of one AddOrReplace (optional): status of the add that carried it,
+    // called on the worker thread (the reference awaits each add, usearch.rs:230-232)
+    using AddDone = void (*)(void* ctx, uint64_t key, int status);
+
     struct Msg {
         Kind kind;
         uint64_t key = 0;
         size_t k = 0;
         std::vector<float> vec;
         Waiter* w = nullptr;
+        AddDone done = nullptr;
+        void* done_ctx = nullptr;
     };
 
     Actor(std::unique_ptr<ActorBackend> be, const ActorConfig& cfg) : be_(std::move(be)), cfg_(cfg) {
@@ -143,10 +149,12 @@ class Actor {
     size_t dimensions() const { return be_->dimensions(); }
 
     // Index::AddOrReplace — fire and forget, like the reference's channel send
-    void add_or_replace(uint64_t key, const float* vec) {
+    void add_or_replace(uint64_t key, const float* vec, AddDone done = nullptr, void* done_ctx = nullptr) {
         Msg m;
         m.kind = ADD;
         m.key = key;
+        m.done = done;
+        m.done_ctx = done_ctx;
         m.vec.assign(vec, vec + be_->dimensions());
         push(std::move(m));
     }
@@ -190,6 +198,10 @@ class Actor {
         if (out) *out = w.count;
         return rc;
     }
+
+    // live size now, without waiting for queued writes: the reference's count is a
+    // read-lock size() beside its fire-and-forget adds (usearch.rs:308-311)
+    size_t size_now() const { return be_->size(); }
 
     // wait until every message submitted before this call has been applied
     int flush() {
@@ -278,11 +290,13 @@ class Actor {
         std::vector<uint64_t> rm, add;
         std::vector<float> vecs;
         std::unordered_set<uint64_t> touched;
+        std::vector<std::pair<AddDone, void*>> done;  // per add
         void clear() {
             rm.clear();
             add.clear();
             vecs.clear();
             touched.clear();
+            done.clear();
         }
     };
 
@@ -303,6 +317,7 @@ class Actor {
                 if (be_->contains(m.key)) s.rm.push_back(m.key);  // replace, usearch.rs:214-219
                 s.add.push_back(m.key);
                 s.vecs.insert(s.vecs.end(), m.vec.begin(), m.vec.begin() + d);
+                s.done.emplace_back(m.done, m.done_ctx);
             }
         }
         apply(s);
@@ -327,10 +342,14 @@ class Actor {
                 ctr_.reserve_calls++;
             }
             if (rc == 0) rc = be_->add(s.add.data(), s.vecs.data(), s.add.size());
-            std::lock_guard<std::mutex> lk(cm_);
-            ctr_.add_calls++;
-            ctr_.max_add_batch = std::max<uint64_t>(ctr_.max_add_batch, s.add.size());
-            if (rc) ctr_.add_errors += s.add.size();
+            {
+                std::lock_guard<std::mutex> lk(cm_);
+                ctr_.add_calls++;
+                ctr_.max_add_batch = std::max<uint64_t>(ctr_.max_add_batch, s.add.size());
+                if (rc) ctr_.add_errors += s.add.size();
+            }
+            for (size_t i = 0; i < n; ++i)
+                if (s.done[i].first) s.done[i].first(s.done[i].second, s.add[i], rc);
         }
         s.clear();
     }

@@ -20,11 +20,13 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
 #include "../../include/vsg.h"
 #include "keymap.hpp"
+#include "roctx_range.hpp"
 #include "vsg_kernels.hpp"
 
 namespace vsg {
@@ -130,7 +132,14 @@ void host_parallel(size_t n, F&& f) {
     }
     std::vector<std::thread> th;
     const size_t step = (n + T - 1) / T;
-    for (size_t lo = 0; lo < n; lo += step) th.emplace_back([&f, lo, n, step] { f(lo, std::min(n, lo + step)); });
+    size_t lo = 0;
+    // a thread that cannot be started (thread or pids limit) must not throw
+    // across the C ABI: the ranges not handed out run on this thread
+    try {
+        for (; lo < n; lo += step) th.emplace_back([&f, lo, n, step] { f(lo, std::min(n, lo + step)); });
+    } catch (const std::system_error&) {
+    }
+    for (; lo < n; lo += step) f(lo, std::min(n, lo + step));
     for (auto& t : th) t.join();
 }
 
@@ -193,6 +202,60 @@ struct Workspace {
     }
 };
 
+// Device-resident searches (vsg_index_search_device, _exact_search_device) are
+// enqueued on the caller's stream and return before they run.  Each records a
+// completion event here; a writer that frees or rewrites memory such a search
+// may still read -- capacity or upper-table growth, compaction, the f16 copy's
+// reallocation -- first waits for all of them (include/vsg.h, "Device-resident
+// variants").  Appends and tombstones need no wait: a running search sees a
+// prefix of them, as with the host API.
+struct SearchFence {
+    std::mutex m;
+    std::vector<hipEvent_t> pending, idle;
+    hipError_t record(hipStream_t s) {
+        hipEvent_t e = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(m);
+            for (size_t i = 0; i < pending.size();) {  // recycle completed events
+                if (hipEventQuery(pending[i]) == hipSuccess) {
+                    idle.push_back(pending[i]);
+                    pending[i] = pending.back();
+                    pending.pop_back();
+                } else {
+                    ++i;
+                }
+            }
+            if (!idle.empty()) {
+                e = idle.back();
+                idle.pop_back();
+            }
+        }
+        if (!e) {
+            const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+            if (r != hipSuccess) return r;
+        }
+        const hipError_t r = hipEventRecord(e, s);
+        std::lock_guard<std::mutex> lk(m);
+        (r == hipSuccess ? pending : idle).push_back(e);
+        return r;
+    }
+    // caller holds the index lock exclusively: no search can enqueue meanwhile
+    void drain() {
+        std::vector<hipEvent_t> p;
+        {
+            std::lock_guard<std::mutex> lk(m);
+            p.swap(pending);
+        }
+        for (hipEvent_t e : p) (void)hipEventSynchronize(e);
+        std::lock_guard<std::mutex> lk(m);
+        idle.insert(idle.end(), p.begin(), p.end());
+    }
+    ~SearchFence() {
+        drain();
+        for (hipEvent_t e : idle) (void)hipEventDestroy(e);
+    }
+};
+
 struct vsg_index {
     vsg_index_options_t opt{};
     int dim = 0;
@@ -234,7 +297,9 @@ struct vsg_index {
     // device time of the build kernels (writer side): events recorded around each
     // batch's insert / sort / reverse launches, read after the call's final sync
     std::vector<hipEvent_t> ev_pool;
-    uint64_t t_insert_ns = 0, t_sort_ns = 0, t_reverse_ns = 0;
+    std::atomic<uint64_t> t_insert_ns{0}, t_sort_ns{0}, t_reverse_ns{0};
+    // device-resident searches still enqueued on caller streams (SearchFence)
+    SearchFence fence;
 
     // build workspace (writer side only)
     int8_t* d_blevels = nullptr;
@@ -361,6 +426,7 @@ static int grow_array(X** arr, size_t used, size_t newcap, int fill, hipStream_t
 static int reserve_locked(vsg_index* h, size_t capacity) {
     if (capacity <= h->cap) return VSG_OK;
     if (capacity > MAX_SLOTS) return fail(VSG_EINVAL, "capacity exceeds 2^29 slots per shard");
+    h->fence.drain();  // enqueued device searches read the arrays freed below
     const size_t s = h->slots;
     uint8_t* nv = nullptr;
     HIP_TRY(dev_alloc(&nv, capacity * h->row_bytes));
@@ -384,6 +450,7 @@ static int ensure_upper(vsg_index* h, size_t rows) {
     if (rows <= h->upper_cap) return VSG_OK;
     size_t want = std::max<size_t>(h->upper_cap * 2, 1024);
     while (want < rows) want *= 2;
+    h->fence.drain();
     int rc = grow_array(&h->d_upper, h->upper_used * h->M, want * h->M, 0xFF, h->stream);
     if (rc) return rc;
     h->upper_cap = want;
@@ -988,6 +1055,34 @@ static int validate_graph(size_t slots, const int8_t* levels, const uint32_t* up
     return VSG_OK;
 }
 
+// Every id in slot s's level-l upper row must itself reach level l: the kernels
+// follow it with row(id, l) = upper[upper_off[id] + l - 1], which is EMPTY-offset
+// garbage for a node of a lower level.  Needs validate_graph and adj_ids_ok first
+// (ids < slots, upper rows of each slot inside the table).
+static bool upper_levels_ok(size_t slots, const int8_t* levels, const uint32_t* upper_off, const uint32_t* upper,
+                            size_t M) {
+    for (size_t s = 0; s < slots; ++s) {
+        for (int l = 1; l <= levels[s]; ++l) {
+            const uint32_t* row = upper + ((size_t)upper_off[s] + (size_t)l - 1) * M;
+            for (size_t j = 0; j < M && row[j] != 0xFFFFFFFFu; ++j)
+                if (levels[row[j]] < l) return false;
+        }
+    }
+    return true;
+}
+
+namespace vsg {
+// first i whose key is live in the index, or n (the sharded add's pre-check,
+// vsg_sharded.cpp: every shard is checked before any shard inserts)
+size_t index_first_live(const vsg_index_t* h, const uint64_t* keys, size_t n) {
+    std::shared_lock<std::shared_mutex> lk(h->mu);
+    for (size_t i = 0; i < n; ++i)
+        if (h->keys.find(keys[i], nullptr)) return i;
+    return n;
+}
+int index_device(const vsg_index_t* h) { return h->device; }
+}  // namespace vsg
+
 // ----------------------------------------------------------------- C ABI --
 
 extern "C" {
@@ -1000,6 +1095,7 @@ int vsg_sample_level(uint64_t seed, uint64_t slot, uint32_t connectivity) {
 }
 
 int vsg_index_new(const vsg_index_options_t* o, vsg_index_t** out) {
+    VSG_RANGE();
     if (!o || !out) return fail(VSG_EINVAL, "null argument");
     *out = nullptr;
     if (o->dimensions == 0) return fail(VSG_EINVAL, "dimensions == 0");
@@ -1063,6 +1159,7 @@ int vsg_index_new(const vsg_index_options_t* o, vsg_index_t** out) {
 }
 
 void vsg_index_free(vsg_index_t* h) {
+    VSG_RANGE();
     if (!h) return;
     {
         DeviceGuard dg(h->device);
@@ -1074,6 +1171,7 @@ void vsg_index_free(vsg_index_t* h) {
 }
 
 int vsg_index_reserve(vsg_index_t* h, size_t capacity) {
+    VSG_RANGE();
     if (!h) return fail(VSG_EINVAL, "null index");
     std::lock_guard<std::mutex> wl(h->wmu);
     std::unique_lock<std::shared_mutex> lk(h->mu);
@@ -1180,15 +1278,18 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
 }
 
 int vsg_index_add(vsg_index_t* h, const uint64_t* keys, const float* vectors, size_t n) {
+    VSG_RANGE();
     return add_common(h, keys, vectors, n, false, nullptr);
 }
 
 int vsg_index_add_device(vsg_index_t* h, const uint64_t* keys, const float* vectors_device, size_t n,
                          void* stream) {
+    VSG_RANGE();
     return add_common(h, keys, vectors_device, n, true, (hipStream_t)stream);
 }
 
 int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_removed) {
+    VSG_RANGE();
     if (!h || (!keys && n)) return fail(VSG_EINVAL, "null argument");
     std::lock_guard<std::mutex> wl(h->wmu);
     std::unique_lock<std::shared_mutex> lk(h->mu);
@@ -1283,15 +1384,18 @@ static int ensure_shadow(vsg_index* h, hipStream_t s) {
     const size_t slots = h->pub_slots;
     if (h->shadow_gen != h->vec_gen || h->shadow_cap < slots || h->shadow_rows > slots) {
         if (h->shadow_cap < h->cap) {
+            h->fence.drain();  // device searches enqueued earlier may walk the old copy
             hipFree(h->d_vecs16);
             h->d_vecs16 = nullptr;
             h->shadow_cap = 0;
             HIP_TRY(dev_alloc(&h->d_vecs16, h->cap * h->row_bytes16));
-            // zeros: a search beside a build may reach rows of the batch in flight
-            // before they are converted (their f32 re-rank is exact either way)
-            HIP_TRY(hipMemsetAsync(h->d_vecs16, 0, h->cap * h->row_bytes16, s));
             h->shadow_cap = h->cap;
         }
+        // zeros past the published rows: a search beside a build may reach rows of
+        // the batch in flight before they are converted (their f32 re-rank is exact
+        // either way); after a compaction those rows still hold pre-compaction images
+        if (h->shadow_cap > slots)
+            HIP_TRY(hipMemsetAsync(h->d_vecs16 + slots * h->row_bytes16, 0, (h->shadow_cap - slots) * h->row_bytes16, s));
         h->shadow_rows = 0;
         h->shadow_gen = h->vec_gen;
     }
@@ -1608,6 +1712,7 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
 
 int vsg_index_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
                      float* out_distances, size_t* out_counts) {
+    VSG_RANGE();
     return search_host(h, queries, nq, k, ef, out_keys, out_distances, out_counts, false);
 }
 
@@ -1620,6 +1725,7 @@ int vsg_index_set_upper_ef(vsg_index_t* h, size_t upper_ef) {
 }
 
 int vsg_index_set_f16_traversal(vsg_index_t* h, int enable) {
+    VSG_RANGE();
     if (!h) return fail(VSG_EINVAL, "null index");
     std::unique_lock<std::shared_mutex> lk(h->mu);
     if (enable && h->st != ST_F32) return fail(VSG_EINVAL, "f16 traversal needs f32 storage");
@@ -1640,27 +1746,35 @@ int vsg_index_set_f16_traversal(vsg_index_t* h, int enable) {
 
 int vsg_index_exact_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, uint64_t* out_keys,
                            float* out_distances, size_t* out_counts) {
+    VSG_RANGE();
     return search_host(h, queries, nq, k, 0, out_keys, out_distances, out_counts, true);
 }
 
 int vsg_index_search_device(vsg_index_t* h, const float* q, size_t nq, size_t k, size_t ef, uint64_t* ok,
                             float* od, uint32_t* oc, void* stream) {
+    VSG_RANGE();
     if (!h) return fail(VSG_EINVAL, "null index");
     std::shared_lock<std::shared_mutex> lk(h->mu);
     DeviceGuard dg(h->device);
-    return search_device_locked(h, q, nq, k, ef, ok, od, oc, (hipStream_t)stream, false);
+    const int rc = search_device_locked(h, q, nq, k, ef, ok, od, oc, (hipStream_t)stream, false);
+    if (rc == VSG_OK && nq) HIP_TRY(h->fence.record((hipStream_t)stream));
+    return rc;
 }
 
 int vsg_index_exact_search_device(vsg_index_t* h, const float* q, size_t nq, size_t k, uint64_t* ok, float* od,
                                   uint32_t* oc, void* stream) {
+    VSG_RANGE();
     if (!h) return fail(VSG_EINVAL, "null index");
     std::shared_lock<std::shared_mutex> lk(h->mu);
     DeviceGuard dg(h->device);
-    return search_device_locked(h, q, nq, k, 0, ok, od, oc, (hipStream_t)stream, true);
+    const int rc = search_device_locked(h, q, nq, k, 0, ok, od, oc, (hipStream_t)stream, true);
+    if (rc == VSG_OK && nq) HIP_TRY(h->fence.record((hipStream_t)stream));
+    return rc;
 }
 
 int vsg_merge_topk_device(const uint64_t* keys, const float* dist, size_t parts, size_t nq, size_t k_in,
                           size_t k_out, uint64_t* out_keys, float* out_dist, void* stream) {
+    VSG_RANGE();
     if (parts == 0 || parts > 64) return fail(VSG_EINVAL, "parts must be in [1, 64]");
     if (k_in == 0 || k_out == 0) return fail(VSG_EINVAL, "k must be >= 1");
     HIP_TRY(launch_merge_topk64(keys, dist, (int)parts, (int)nq, (int)k_in, (int)k_out, out_keys, out_dist,
@@ -1706,7 +1820,9 @@ int vsg_index_reset_stats(vsg_index_t* h) {
     HIP_TRY(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
     h->build_vectors = 0;
     h->build_batches = 0;
-    h->t_insert_ns = h->t_sort_ns = h->t_reverse_ns = 0;
+    h->t_insert_ns = 0;
+    h->t_sort_ns = 0;
+    h->t_reverse_ns = 0;
     return VSG_OK;
 }
 
@@ -1724,6 +1840,7 @@ int vsg_index_graph_info(const vsg_index_t* h, size_t* slots, size_t* upper_rows
 
 int vsg_index_export(const vsg_index_t* h, float* vectors, uint64_t* keys, uint8_t* removed, int8_t* levels,
                      uint32_t* adj0, uint32_t* upper_off, uint32_t* upper) {
+    VSG_RANGE();
     if (!h) return fail(VSG_EINVAL, "null index");
     std::lock_guard<std::mutex> wl(h->wmu);  // no build in flight: a consistent image
     std::shared_lock<std::shared_mutex> lk(h->mu);
@@ -1754,6 +1871,7 @@ int vsg_index_export(const vsg_index_t* h, float* vectors, uint64_t* keys, uint8
 int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const uint64_t* keys,
                      const uint8_t* removed, const int8_t* levels, const uint32_t* adj0, const uint32_t* upper_off,
                      const uint32_t* upper, size_t upper_rows, uint32_t entry, int max_level) {
+    VSG_RANGE();
     if (!h) return fail(VSG_EINVAL, "null index");
     std::lock_guard<std::mutex> wl(h->wmu);
     std::unique_lock<std::shared_mutex> lk(h->mu);
@@ -1768,6 +1886,8 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
     if (rc) return rc;
     if (!adj_ids_ok(adj0, slots * h->M0, slots, h->M0) || !adj_ids_ok(upper, upper_rows * h->M, slots, h->M))
         return fail(VSG_EINVAL, "import: adjacency id out of range");
+    if (!(h->opt.flags & VSG_FLAG_EXACT_ONLY) && !upper_levels_ok(slots, levels, upper_off, upper, h->M))
+        return fail(VSG_EINVAL, "import: an upper-level row links a node below that level");
     {
         KeyMap probe;
         probe.reserve(slots);
@@ -1813,6 +1933,7 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
 // build.  Relative slot order is kept, so exact-search ties resolve as before.
 
 int vsg_index_compact(vsg_index_t* h, size_t* n_dropped) {
+    VSG_RANGE();
     if (!h) return fail(VSG_EINVAL, "null index");
     if (n_dropped) *n_dropped = 0;
     std::lock_guard<std::mutex> wl(h->wmu);
@@ -1820,6 +1941,7 @@ int vsg_index_compact(vsg_index_t* h, size_t* n_dropped) {
     DeviceGuard dg(h->device);
     const size_t s = h->slots;
     if (s == h->live) return VSG_OK;
+    h->fence.drain();  // rows move and the graph is rewritten in place
     hipStream_t st = h->stream;
     std::vector<uint8_t> fl(s);
     HIP_TRY(hipMemcpyAsync(fl.data(), h->d_flags, s, hipMemcpyDeviceToHost, st));
@@ -1977,6 +2099,7 @@ constexpr size_t kIoChunk = (size_t)16 << 20;
 extern "C" {
 
 int vsg_index_save(const vsg_index_t* h, const char* path) {
+    VSG_RANGE();
     if (!h || !path) return fail(VSG_EINVAL, "null argument");
     std::lock_guard<std::mutex> wl(h->wmu);
     std::shared_lock<std::shared_mutex> lk(h->mu);
@@ -2051,6 +2174,7 @@ int vsg_index_file_info(const char* path, vsg_file_info_t* out) {
 }
 
 int vsg_index_load(const char* path, int device, vsg_index_t** out) {
+    VSG_RANGE();
     if (!path || !out) return fail(VSG_EINVAL, "null argument");
     *out = nullptr;
     FileCloser fc{std::fopen(path, "rb")};
@@ -2077,6 +2201,7 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
     std::vector<uint64_t> keys(s);
     std::vector<uint8_t> flags(s);
     std::vector<uint32_t> uoff(s);
+    std::vector<uint32_t> upper_h(fh.upper_rows * fh.M);  // host copy for upper_levels_ok
     PinnedBuf buf;
     HIP_TRY(hipHostMalloc((void**)&buf.p, kIoChunk, hipHostMallocDefault));
     Fnv hash;
@@ -2097,6 +2222,7 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
             if (si == 3) std::memcpy(flags.data() + off, buf.p, c);
             if (si == 4) std::memcpy(reinterpret_cast<uint8_t*>(h->h_levels.data()) + off, buf.p, c);
             if (si == 6) std::memcpy(reinterpret_cast<uint8_t*>(uoff.data()) + off, buf.p, c);
+            if (si == 7) std::memcpy(reinterpret_cast<uint8_t*>(upper_h.data()) + off, buf.p, c);
             if ((si == 5 || si == 7) && !adj_ids_ok(reinterpret_cast<const uint32_t*>(buf.p), c / 4, s,
                                                      si == 5 ? fh.M0 : fh.M, off / 4, &prev_empty))
                 return fail(VSG_EINVAL, "vsg index file: adjacency id out of range");
@@ -2105,6 +2231,8 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
     if (hash.h != fh.payload_hash) return fail(VSG_EINVAL, "vsg index file payload checksum mismatch");
     if ((rc = validate_graph(s, h->h_levels.data(), uoff.data(), fh.upper_rows, fh.entry, fh.max_level,
                                  (h->opt.flags & VSG_FLAG_EXACT_ONLY) != 0))) return rc;
+    if (!(h->opt.flags & VSG_FLAG_EXACT_ONLY) && !upper_levels_ok(s, h->h_levels.data(), uoff.data(), upper_h.data(), fh.M))
+        return fail(VSG_EINVAL, "vsg index file: an upper-level row links a node below that level");
     h->slots = s;
     h->upper_used = fh.upper_rows;
     h->entry = fh.entry;
@@ -2126,6 +2254,7 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
 
 int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed, size_t start_row,
                        float* out, void* stream) {
+    VSG_RANGE();
     if (kind < 0 || kind > 3 || dim == 0) return fail(VSG_EINVAL, "bad datagen arguments");
     hipStream_t s = (hipStream_t)stream;
     float *w = nullptr, *c = nullptr;

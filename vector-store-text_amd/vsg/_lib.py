@@ -96,6 +96,19 @@ class ActorOptions(C.Structure):
     ]
 
 
+class ShardedOptions(C.Structure):
+    _fields_ = [
+        ("index", Options),
+        ("n_shards", C.c_uint32),
+        ("answer_device", C.c_int32),
+        ("devices", C.POINTER(C.c_int32)),
+    ]
+
+
+# void (*)(void* ctx, uint64_t key, int status): vsg_actor_add_or_replace_cb completion
+ADD_DONE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64, C.c_int)
+
+
 class ActorCounters(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in (
         "messages", "writes", "anns", "counts", "add_calls", "remove_calls", "search_calls",
@@ -167,6 +180,28 @@ def lib() -> C.CDLL:
         "vsg_actor_flush": (C.c_int, [P]),
         "vsg_actor_counters": (C.c_int, [P, C.POINTER(ActorCounters)]),
         "vsg_actor_index": (P, [P]),
+        "vsg_actor_sharded": (P, [P]),
+        "vsg_actor_new_sharded": (C.c_int, [C.POINTER(ActorOptions), u32, P, C.POINTER(P)]),
+        "vsg_actor_add_or_replace_cb": (C.c_int, [P, u64, P, sz, ADD_DONE_FN, P]),
+        "vsg_actor_size": (sz, [P]),
+        "vsg_sharded_new": (C.c_int, [C.POINTER(ShardedOptions), C.POINTER(P)]),
+        "vsg_sharded_free": (None, [P]),
+        "vsg_sharded_reserve": (C.c_int, [P, sz]),
+        "vsg_sharded_capacity": (sz, [P]),
+        "vsg_sharded_size": (sz, [P]),
+        "vsg_sharded_dimensions": (sz, [P]),
+        "vsg_sharded_contains": (C.c_int, [P, u64]),
+        "vsg_sharded_shard_count": (sz, [P]),
+        "vsg_sharded_route": (u32, [P, u64]),
+        "vsg_sharded_shard": (P, [P, sz]),
+        "vsg_sharded_add": (C.c_int, [P, P, P, sz]),
+        "vsg_sharded_remove": (C.c_int, [P, P, sz, C.POINTER(sz)]),
+        "vsg_sharded_search": (C.c_int, [P, P, sz, sz, sz, P, P, P]),
+        "vsg_sharded_exact_search": (C.c_int, [P, P, sz, sz, P, P, P]),
+        "vsg_sharded_search_device": (C.c_int, [P, P, sz, sz, sz, C.c_int, P, P, P]),
+        "vsg_sharded_compact": (C.c_int, [P, C.POINTER(sz)]),
+        "vsg_sharded_stats": (C.c_int, [P, C.POINTER(Stats)]),
+        "vsg_sharded_reset_stats": (C.c_int, [P]),
         "vsg_last_error": (C.c_char_p, []),
         "vsg_version": (C.c_char_p, []),
     }

@@ -18,7 +18,8 @@ from typing import Hashable, Sequence
 
 import numpy as np
 
-from ._lib import METRICS, NO_KEY, SCALARS, ActorCounters, ActorOptions, Options, Stats, VsgError, check, lib
+from ._lib import (ADD_DONE_FN, METRICS, NO_KEY, SCALARS, ActorCounters, ActorOptions, Options, Stats, VsgError,
+                   check, lib)
 
 
 class Actor:
@@ -28,7 +29,9 @@ class Actor:
                  connectivity: int = 0, expansion_add: int = 0, expansion_search: int = 0,
                  device: int = 0, seed: int = 0, reserve_increment: int = 0, reserve_threshold: int = 0,
                  max_batch: int = 0, max_wait_us: int = 0, compact_percent: int = 0, compact_min_dead: int = 0,
-                 f16_traversal: bool = False, concurrent_reads: bool = False):
+                 f16_traversal: bool = False, concurrent_reads: bool = False, devices=None):
+        """devices: a list of device ordinals => one shard per entry (vsg_actor_new_sharded,
+        include/vsg.h "Sharded index"); None => one index on `device`."""
         self.dimensions = int(dimensions)
         # f16_traversal: opt-in VSG_FLAG_F16_TRAVERSAL (f16 walk + exact f32 re-rank, DESIGN.md §3.5)
         opt = ActorOptions(Options(self.dimensions, METRICS[metric], SCALARS[quantization], connectivity,
@@ -36,8 +39,13 @@ class Actor:
                            reserve_increment, reserve_threshold, max_batch, max_wait_us, compact_percent,
                            1 if concurrent_reads else 0, compact_min_dead)
         h = C.c_void_p()
-        check(lib().vsg_actor_new(C.byref(opt), C.byref(h)))
+        if devices is None:
+            check(lib().vsg_actor_new(C.byref(opt), C.byref(h)))
+        else:
+            devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+            check(lib().vsg_actor_new_sharded(C.byref(opt), len(devices), C.cast(devs, C.c_void_p), C.byref(h)))
         self._h = h
+        self.sharded = devices is not None
 
     def close(self) -> None:
         h = getattr(self, "_h", None)
@@ -51,9 +59,19 @@ class Actor:
         except Exception:
             pass
 
-    def add_or_replace(self, key: int, embedding) -> None:
+    def add_or_replace(self, key: int, embedding, done=None) -> None:
+        """done: optional ADD_DONE_FN(ctx, key, status), called on the worker thread when
+        the batched add carrying this message finished (keep it referenced until then)."""
         v = np.ascontiguousarray(embedding, dtype=np.float32).reshape(-1)
-        check(lib().vsg_actor_add_or_replace(self._h, int(key), C.c_void_p(v.ctypes.data), v.size))
+        if done is None:
+            check(lib().vsg_actor_add_or_replace(self._h, int(key), C.c_void_p(v.ctypes.data), v.size))
+        else:
+            check(lib().vsg_actor_add_or_replace_cb(self._h, int(key), C.c_void_p(v.ctypes.data), v.size, done,
+                                                    None))
+
+    def size_now(self) -> int:
+        """Live size without waiting for queued writes (the reference's count, usearch.rs:308-311)."""
+        return lib().vsg_actor_size(self._h)
 
     def remove(self, key: int) -> None:
         check(lib().vsg_actor_remove(self._h, int(key)))
@@ -82,11 +100,16 @@ class Actor:
         return {f: getattr(c, f) for f, _ in ActorCounters._fields_}
 
     def capacity(self) -> int:
+        if self.sharded:
+            return lib().vsg_sharded_capacity(lib().vsg_actor_sharded(self._h))
         return lib().vsg_index_capacity(lib().vsg_actor_index(self._h))
 
     def index_stats(self) -> dict:
         s = Stats()
-        check(lib().vsg_index_stats(lib().vsg_actor_index(self._h), C.byref(s)))
+        if self.sharded:
+            check(lib().vsg_sharded_stats(lib().vsg_actor_sharded(self._h), C.byref(s)))
+        else:
+            check(lib().vsg_index_stats(lib().vsg_actor_index(self._h), C.byref(s)))
         return {f: getattr(s, f) for f, _ in Stats._fields_}
 
 
@@ -105,6 +128,18 @@ class UsearchIndex:
         self._pk2key: dict = {}
         self._key2pk: dict = {}
         self._next = 0  # usearch_key AtomicU64, usearch.rs:113
+        # a failed add drops the PK <-> key mapping again (usearch.rs:230-232)
+        self._done = ADD_DONE_FN(self._add_done)
+        self.failed_adds = 0
+
+    def _add_done(self, _ctx, key, status):
+        if status == 0:
+            return
+        with self._lock:
+            self.failed_adds += 1
+            pk = self._key2pk.pop(key, None)
+            if pk is not None and self._pk2key.get(pk) == key:
+                del self._pk2key[pk]
 
     # usearch.rs:174-233
     def add_or_replace(self, primary_key: Hashable, embedding: Sequence[float]) -> None:
@@ -115,7 +150,8 @@ class UsearchIndex:
                 self._next += 1
                 self._pk2key[primary_key] = key
                 self._key2pk[key] = primary_key
-        self.actor.add_or_replace(key, embedding)  # replace: the actor removes the live key first
+        # replace: the actor removes the live key first
+        self.actor.add_or_replace(key, embedding, done=self._done)
 
     # usearch.rs:235-249
     def remove(self, primary_key: Hashable) -> None:

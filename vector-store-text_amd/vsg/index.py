@@ -63,11 +63,20 @@ class Index:
         self._h = h
         self.device = device
 
+    @classmethod
+    def _borrowed(cls, handle, dimensions, metric, quantization, device, owner=None) -> "Index":
+        """Non-owning view of a shard handle (ShardedIndex.shard); `owner` is kept alive."""
+        self = cls.__new__(cls)
+        self._h = C.c_void_p(handle)
+        self._owner = owner
+        self.dimensions, self.metric, self.quantization, self.device = int(dimensions), metric, quantization, device
+        return self
+
     def close(self):
         h = getattr(self, "_h", None)
-        if h:
+        if h and getattr(self, "_owner", None) is None:
             lib().vsg_index_free(h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:

@@ -97,6 +97,7 @@ typedef struct {
     uint64_t build_insert_ns;          /* device time of the build kernels (HIP events on the build */
     uint64_t build_sort_ns;            /*   stream): insert (descent + beam + selection), pair sort, */
     uint64_t build_reverse_ns;         /*   reverse links -- the build roofline's time base */
+    uint64_t build_select_ns;          /* the selection kernel's share of build_insert_ns (split insert) */
 } vsg_stats_t;
 
 /* replaces usearch::Index::new(&options) — src/index/usearch.rs:98 */

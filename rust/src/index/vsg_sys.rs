@@ -70,6 +70,7 @@ pub struct vsg_stats_t {
     pub build_insert_ns: u64,
     pub build_sort_ns: u64,
     pub build_reverse_ns: u64,
+    pub build_select_ns: u64,
 }
 
 /// The native actor's options (src/index/usearch.rs:60-66, 101-118 constants made knobs).

@@ -118,14 +118,31 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
 #ifndef VSG_SEL_VGPRS
 #define VSG_SEL_VGPRS 96
 #endif
+// SU: row passes in flight per kept-set test (rows_test U), capped at the
+// shape's U.  The test is a chain of dependent L2 round trips (the kept rows
+// were fetched by the beam moments ago): more passes per trip, fewer trips.
 #ifndef VSG_SEL_U
 #define VSG_SEL_U 1
 #endif
-template <int G, int VM, int U, typename T, int MET>
+// occupancy requests of the selection / reverse kernels (probes: e.g.
+// -DVSG_SEL_WAVES='__attribute__((amdgpu_waves_per_eu(3, 3)))')
+#ifndef VSG_SEL_WAVES
+#define VSG_SEL_WAVES
+#endif
+#ifndef VSG_REV_WAVES
+#define VSG_REV_WAVES
+#endif
+#ifndef VSG_SEL_U_INSERT
+#define VSG_SEL_U_INSERT VSG_SEL_U
+#endif
+#ifndef VSG_SEL_U_REVERSE
+#define VSG_SEL_U_REVERSE VSG_SEL_U
+#endif
+template <int G, int VM, int U, typename T, int MET, int SU = VSG_SEL_U>
 __device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uint64_t& ndist) {
     constexpr int QF = VM * ChunkT<T>::E;
     constexpr int NQ = QF * 4 <= VSG_SEL_VGPRS ? 4 : QF * 3 <= VSG_SEL_VGPRS ? 3 : QF * 2 <= VSG_SEL_VGPRS ? 2 : 1;
-    constexpr int UT = VSG_SEL_U < U ? VSG_SEL_U : U;  // row passes in flight per test
+    constexpr int UT = SU;  // row passes in flight per test
     constexpr int BLK = (64 / G) * UT;
     const int lane = lane_id();
     List& L = w.list;
@@ -172,6 +189,19 @@ __device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uin
         wave_sync();
     }
     return kept;
+}
+
+// The selected neighbours (and, when the graph carries them, their distances
+// to `node`: the values the selection walked, kept so the reverse-link prune
+// need not recompute them) become row(node, l); EMPTY / +inf past nsel.
+__device__ inline void write_row(const GraphDev& g, uint32_t node, int l, int m, int nsel, const WaveLds& w) {
+    const int lane = lane_id();
+    uint32_t* row = g.row(node, l);
+    for (int j = lane; j < m; j += 64) row[j] = j < nsel ? w.sel[j] : VSG_EMPTY;
+    if (g.adjd0) {
+        float* rd = g.rowd(node, l);
+        for (int j = lane; j < m; j += 64) rd[j] = j < nsel ? w.seld[j] : __builtin_inff();
+    }
 }
 
 // ------------------------------------------------------------------ search --
@@ -444,8 +474,7 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
         const uint64_t ts = VSG_CLK();
         const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, m, nsel_d);
         tsel += VSG_CLK() - ts;
-        uint32_t* row = g.row(node, l);
-        for (int j = lane; j < m; j += 64) row[j] = j < nsel ? w.sel[j] : VSG_EMPTY;
+        write_row(g, node, l, m, nsel, w);
         for (int j = lane; j < nsel; j += 64) {
             const uint64_t key = ((uint64_t)l << PAIR_L_SHIFT) | ((uint64_t)w.sel[j] << PAIR_V_SHIFT) |
                                  (uint64_t)node;
@@ -535,7 +564,7 @@ __global__ __launch_bounds__(64) void hnsw_insert_beam_kernel(InsertParams p) {
 }
 
 template <int G, int VM, int U, typename T, int MET>
-__global__ __launch_bounds__(64) void hnsw_insert_select_kernel(InsertParams p) {
+__global__ __launch_bounds__(64) VSG_SEL_WAVES void hnsw_insert_select_kernel(InsertParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int bi = insert_index(p);
     const int lane = lane_id();
@@ -558,9 +587,8 @@ __global__ __launch_bounds__(64) void hnsw_insert_select_kernel(InsertParams p) 
         w.list.size = n;
         wave_sync();
         const int m = l == 0 ? g.M0 : g.M;
-        const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, n, m, nsel_d);
-        uint32_t* row = g.row(node, l);
-        for (int j = lane; j < m; j += 64) row[j] = j < nsel ? w.sel[j] : VSG_EMPTY;
+        const int nsel = select_heuristic<G, VM, U, T, MET, VSG_SEL_U_INSERT>(g, w, n, m, nsel_d);
+        write_row(g, node, l, m, nsel, w);
         for (int j = lane; j < nsel; j += 64) {
             const uint64_t key = ((uint64_t)l << PAIR_L_SHIFT) | ((uint64_t)w.sel[j] << PAIR_V_SHIFT) |
                                  (uint64_t)node;
@@ -581,13 +609,17 @@ __global__ __launch_bounds__(64) void hnsw_insert_select_kernel(InsertParams p) 
 // segment heads; each segment (level, v) is merged into v's row: append while
 // there is room, else heuristic re-selection over existing + incoming.
 
+// One instance for both paths (stored distances / recomputed): compiled as two
+// instances, the stored-distance one got 185 VGPRs instead of 239 and ran 50 %
+// slower (C2 reverse 54 -> 82 ms; profiles/r03_build_probe.jsonl) -- the larger
+// allocation keeps more of the selection's row loads in flight.
 template <int G, int VM, int U, typename T, int MET>
-__global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
+__global__ __launch_bounds__(64) VSG_REV_WAVES void hnsw_reverse_kernel(ReverseParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
     const int cap = 2 * g.M0 > 64 ? 2 * g.M0 : 64;
-    WaveLds w = carve(smem, cap, hash_size_for(cap, 32), sel_entries(g.M0));
+    WaveLds w = carve(smem, cap, 0, sel_entries(g.M0));  // no visited table
     const uint64_t t_start = wall_clock64();
     uint64_t ndist = 0, nadj = 0, nsel_d = 0, nprune = 0, nappend = 0;
     const size_t nw = gridDim.x;
@@ -631,31 +663,47 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
                 ne += popc64(xm);
                 if (xm != ~0ull) break;
             }
+            float* rowd = g.adjd0 ? g.rowd(v, l) : nullptr;
             if (ne + nin <= m) {
-                for (int t = lane; t < nin; t += 64) row[ne + t] = (uint32_t)(p.keys[h + t] & PAIR_ID_MASK);
+                for (int t = lane; t < nin; t += 64) {
+                    row[ne + t] = (uint32_t)(p.keys[h + t] & PAIR_ID_MASK);
+                    if (rowd) rowd[ne + t] = __uint_as_float(p.vals[h + t]);
+                }
                 ++nappend;
                 continue;
             }
             ++nprune;
-            QReg<G, VM, T> q;
-            q.load(g.vec(v), g.nchunks);
             List& L = w.list;
             L.cur = 0;
             L.size = 0;
-            for (int c0 = 0; c0 < ne; c0 += 64) {  // existing neighbours, distances recomputed
-                const uint32_t x = c0 + lane < ne ? row[c0 + lane] : VSG_EMPTY;
-                const uint64_t xm = __ballot(x != VSG_EMPTY);
-                const int c = popc64(xm);
-                if (x != VSG_EMPTY) w.todo[lanes_below(xm)] = x;
-                wave_sync();
-                rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, c, q, w.tdist);
-                wave_sync();
-                ndist += (uint64_t)c;
-                const bool valid = lane < c;
-                const float cd = valid ? w.tdist[lane] : 0.f;
-                const uint32_t ci = valid ? w.todo[lane] : 0u;
-                wave_sync();
-                L.merge(valid, cd, ci, false, w.sd, w.si);
+            if (rowd) {
+                // existing neighbours with their stored distances: the values the
+                // insert that wrote them computed -- dist(v, x) or dist(x, v), the
+                // same float (operand-symmetric: (a-b)^2, a.b, same lane order)
+                for (int c0 = 0; c0 < ne; c0 += 64) {
+                    const bool valid = c0 + lane < ne;
+                    const uint32_t ci = valid ? row[c0 + lane] : 0u;
+                    const float cd = valid ? rowd[c0 + lane] : 0.f;
+                    L.merge(valid, cd, ci, false, w.sd, w.si);
+                }
+            } else {
+                QReg<G, VM, T> q;
+                q.load(g.vec(v), g.nchunks);
+                for (int c0 = 0; c0 < ne; c0 += 64) {  // existing neighbours, distances recomputed
+                    const uint32_t x = c0 + lane < ne ? row[c0 + lane] : VSG_EMPTY;
+                    const uint64_t xm = __ballot(x != VSG_EMPTY);
+                    const int c = popc64(xm);
+                    if (x != VSG_EMPTY) w.todo[lanes_below(xm)] = x;
+                    wave_sync();
+                    rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, c, q, w.tdist);
+                    wave_sync();
+                    ndist += (uint64_t)c;
+                    const bool valid = lane < c;
+                    const float cd = valid ? w.tdist[lane] : 0.f;
+                    const uint32_t ci = valid ? w.todo[lane] : 0u;
+                    wave_sync();
+                    L.merge(valid, cd, ci, false, w.sd, w.si);
+                }
             }
             for (int t = 0; t < nin; t += 64) {
                 const bool valid = t + lane < nin;
@@ -664,8 +712,8 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
                 const uint32_t ci = valid ? (uint32_t)(p.keys[idx] & PAIR_ID_MASK) : 0u;
                 L.merge(valid, cd, ci, false, w.sd, w.si);
             }
-            const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, L.size, m, nsel_d);
-            for (int j = lane; j < m; j += 64) row[j] = j < nsel ? w.sel[j] : VSG_EMPTY;
+            const int nsel = select_heuristic<G, VM, U, T, MET, VSG_SEL_U_REVERSE>(g, w, L.size, m, nsel_d);
+            write_row(g, v, l, m, nsel, w);
             wave_sync();
         }
     }
@@ -680,6 +728,53 @@ __global__ __launch_bounds__(64) void hnsw_reverse_kernel(ReverseParams p) {
         atomicAdd(&p.stats[12], dt);
         atomicMax(&p.stats[13], dt);
     }
+}
+
+// ------------------------------------------------------- edge distances --
+// Per-edge distances of a graph that arrived without them (import, load): one
+// wave per slot, dist(slot, neighbour) for every entry of every level's row --
+// the value rows_dist gives with the slot as query, as the build stores it.
+
+template <int G, int VM, int U, typename T, int MET>
+__global__ __launch_bounds__(64) void edge_dist_fill_kernel(DevGraph gd, const int8_t* levels, uint32_t n) {
+    __shared__ uint32_t todo[64];
+    __shared__ float tdist[64];
+    const uint32_t s = blockIdx.x;
+    if (s >= n) return;
+    const int lane = lane_id();
+    const GraphDev g = to_dev(gd);
+    QReg<G, VM, T> q;
+    q.load(g.vec(s), g.nchunks);
+    for (int l = 0; l <= levels[s]; ++l) {
+        const int m = l == 0 ? g.M0 : g.M;
+        const uint32_t* row = g.row(s, l);
+        float* rd = g.rowd(s, l);
+        for (int c0 = 0; c0 < m; c0 += 64) {
+            const uint32_t x = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
+            const uint64_t xm = __ballot(x != VSG_EMPTY);
+            const int c = popc64(xm);  // compact prefix: the first c lanes
+            if (x != VSG_EMPTY) todo[lane] = x;
+            wave_sync();
+            if (c) rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, todo, c, q, tdist);
+            wave_sync();
+            if (c0 + lane < m) rd[c0 + lane] = lane < c ? tdist[lane] : __builtin_inff();
+            wave_sync();
+            if (xm != ~0ull) break;
+        }
+    }
+}
+
+hipError_t launch_edge_dist_fill(Storage st, MetricKind mk, const DevGraph& g, const int8_t* levels, size_t n,
+                                 hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (!g.adjd0 || !g.upperd) return hipErrorInvalidValue;
+    hipError_t err = hipSuccess;
+    dispatch_all(st, mk, g.nchunks, [&](auto sh, auto tt, auto mt) {
+        auto kern = VSG_KERNEL_OF(edge_dist_fill_kernel, sh, tt, mt);
+        hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(64), 0, s, g, levels, (uint32_t)n);
+        err = hipGetLastError();
+    });
+    return err;
 }
 
 // ------------------------------------------------------------------ launch --
@@ -736,7 +831,7 @@ hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipSt
     return err;
 }
 
-hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s) {
+hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s, hipEvent_t mid) {
     if (p.nnodes <= 0) return hipSuccess;
     if (p.efc > 192 || !p.list_off || !p.lst_d || !p.lst_i || !p.lst_n) return hipErrorInvalidValue;
     const size_t lds_beam = wave_lds_bytes(p.hash_size, p.efc, 0);
@@ -748,6 +843,7 @@ hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p,
         if (lds_beam > 65536) (void)hipFuncSetAttribute((const void*)kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_beam);
         hipLaunchKernelGGL(kb, dim3(p.nnodes), dim3(64), lds_beam, s, p);
         err = hipGetLastError();
+        if (err == hipSuccess && mid) err = hipEventRecord(mid, s);
         if (err == hipSuccess) {
             hipLaunchKernelGGL(ks, dim3(p.nnodes), dim3(64), lds_sel, s, p);
             err = hipGetLastError();
@@ -759,7 +855,7 @@ hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p,
 hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s) {
     if (p.npairs == 0) return hipSuccess;
     const int cap = 2 * p.g.M0 > 64 ? 2 * p.g.M0 : 64;
-    const size_t lds = insert_lds_bytes(cap, hash_size_for(cap, 32), p.g.M0);
+    const size_t lds = insert_lds_bytes(cap, 0, p.g.M0);
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(hnsw_reverse_kernel, sh, tt, mt);

@@ -24,6 +24,8 @@ static __device__ inline GraphDev to_dev(const DevGraph& g) {
     d.upper = g.upper;
     d.M = g.M;
     d.M0 = g.M0;
+    d.adjd0 = g.adjd0;
+    d.upperd = g.upperd;
     return d;
 }
 

@@ -606,9 +606,15 @@ struct GraphDev {
     const uint32_t* upper_off;
     uint32_t* upper;
     int M, M0;
+    float* adjd0;   // per-edge distances (build kernels; nullptr otherwise)
+    float* upperd;
 
     __device__ __forceinline__ uint32_t* row(uint32_t s, int l) const {
         return l == 0 ? adj0 + (size_t)s * M0 : upper + ((size_t)upper_off[s] + (size_t)(l - 1)) * M;
+    }
+    // the distances of row(s, l)'s entries (same layout)
+    __device__ __forceinline__ float* rowd(uint32_t s, int l) const {
+        return l == 0 ? adjd0 + (size_t)s * M0 : upperd + ((size_t)upper_off[s] + (size_t)(l - 1)) * M;
     }
     __device__ __forceinline__ const uint8_t* vec(uint32_t s) const { return vecs + (size_t)s * row_bytes; }
 };

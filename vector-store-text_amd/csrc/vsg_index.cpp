@@ -274,6 +274,12 @@ struct vsg_index {
     uint32_t* d_upper_off = nullptr;
     uint32_t* d_upper = nullptr;
     size_t upper_cap = 0, upper_used = 0;
+    // per-edge distances beside adj0 / upper (build kernels only; DevGraph.adjd0):
+    // written with every row, read by the reverse-link prune instead of
+    // recomputing; an imported or loaded graph has none until the next add fills them
+    float* d_adjd0 = nullptr;
+    float* d_upperd = nullptr;
+    bool adjd_valid = true;
     uint64_t* d_keys = nullptr;
     uint8_t* d_flags = nullptr;
     float* d_sqnorm = nullptr;  // |stored row|^2 (MFMA exact L2 expansion)
@@ -297,7 +303,7 @@ struct vsg_index {
     // device time of the build kernels (writer side): events recorded around each
     // batch's insert / sort / reverse launches, read after the call's final sync
     std::vector<hipEvent_t> ev_pool;
-    std::atomic<uint64_t> t_insert_ns{0}, t_sort_ns{0}, t_reverse_ns{0};
+    std::atomic<uint64_t> t_insert_ns{0}, t_select_ns{0}, t_sort_ns{0}, t_reverse_ns{0};
     // device-resident searches still enqueued on caller streams (SearchFence)
     SearchFence fence;
 
@@ -355,7 +361,8 @@ struct vsg_index {
     uint32_t* d_rm = nullptr;          // remove(): slot list (writer side)
     size_t rm_cap = 0;
 
-    DevGraph graph() const {
+    // searches: adjacency only; builds (with_dist): the per-edge distances too
+    DevGraph graph(bool with_dist = false) const {
         DevGraph g;
         g.vecs = d_vecs;
         g.row_bytes = row_bytes;
@@ -365,6 +372,8 @@ struct vsg_index {
         g.upper = d_upper;
         g.M = M;
         g.M0 = M0;
+        g.adjd0 = with_dist ? d_adjd0 : nullptr;
+        g.upperd = with_dist ? d_upperd : nullptr;
         return g;
     }
 };
@@ -382,6 +391,8 @@ static void free_dev(vsg_index* h) {
     hipFree(h->d_adj0);
     hipFree(h->d_upper_off);
     hipFree(h->d_upper);
+    hipFree(h->d_adjd0);
+    hipFree(h->d_upperd);
     hipFree(h->d_keys);
     hipFree(h->d_flags);
     hipFree(h->d_sqnorm);
@@ -410,6 +421,7 @@ static void free_dev(vsg_index* h) {
     }
 }
 
+
 // grow a device array, copying `used` elements and filling the tail with `fill`
 template <typename X>
 static int grow_array(X** arr, size_t used, size_t newcap, int fill, hipStream_t s) {
@@ -437,6 +449,9 @@ static int reserve_locked(vsg_index* h, size_t capacity) {
     h->vec_gen++;
     int rc;
     if ((rc = grow_array(&h->d_adj0, s * h->M0, capacity * h->M0, 0xFF, h->stream))) return rc;
+    if (!(h->opt.flags & VSG_FLAG_EXACT_ONLY) &&
+        (rc = grow_array(&h->d_adjd0, s * h->M0, capacity * h->M0, 0xFF, h->stream)))
+        return rc;
     if ((rc = grow_array(&h->d_upper_off, s, capacity, 0xFF, h->stream))) return rc;
     if ((rc = grow_array(&h->d_keys, s, capacity, 0xFF, h->stream))) return rc;
     if ((rc = grow_array(&h->d_flags, s, capacity, 0, h->stream))) return rc;
@@ -453,6 +468,9 @@ static int ensure_upper(vsg_index* h, size_t rows) {
     h->fence.drain();
     int rc = grow_array(&h->d_upper, h->upper_used * h->M, want * h->M, 0xFF, h->stream);
     if (rc) return rc;
+    if (!(h->opt.flags & VSG_FLAG_EXACT_ONLY) &&
+        (rc = grow_array(&h->d_upperd, h->upper_used * h->M, want * h->M, 0xFF, h->stream)))
+        return rc;
     h->upper_cap = want;
     return VSG_OK;
 }
@@ -775,6 +793,22 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     }
     if ((rc = ensure_nodes(h, n))) return rc;
     PhaseClock pc;
+    // per-edge distances (VSG_BUILD_EDGE_DIST=0: the reverse prune recomputes
+    // them from the rows -- probes only; the stored ones are then stale)
+    const bool edge_dist = env_double("VSG_BUILD_EDGE_DIST", 1) != 0;
+    if (!edge_dist) h->adjd_valid = false;
+    if (edge_dist && !h->adjd_valid) {
+        // the graph came from import / load: fill the distances of rows [0, s0)
+        if (s0) {
+            int8_t* dl = nullptr;
+            HIP_TRY(dev_alloc(&dl, s0));
+            HIP_TRY(hipMemcpyAsync(dl, h->h_levels.data(), s0, hipMemcpyHostToDevice, st));
+            HIP_TRY(launch_edge_dist_fill(h->st, h->mk, h->graph(true), dl, s0, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            hipFree(dl);
+        }
+        h->adjd_valid = true;
+    }
     // Insertion order = a seeded pseudo-random permutation of the call's slots:
     // nodes of one batch cannot link to each other, so a batch must not be
     // spatially coherent (a cluster-sorted input otherwise wrecks the graph).
@@ -818,13 +852,16 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     // Round 2 sweep at C2 (profiles/r02_build_schedule.jsonl, recall@10 on 10k
     // queries): 1/16 & 32k 1.00 s, recall 0.957; 1/2 & 64k 0.77 s, 0.959 -- the
     // early, latency-bound batches were the cost, and larger ones lose no recall.
-    const double frac = env_double("VSG_BUILD_BATCH_FRAC", 0.5);
-    // probe knobs: a second batch fraction once the graph holds `switch_at` nodes
-    const double frac2 = env_double("VSG_BUILD_BATCH_FRAC2", frac);
-    const double switch_at = env_double("VSG_BUILD_BATCH_SWITCH", 0);
+    // Round 3: while the graph holds < 8,192 nodes a batch is 2x the graph (the
+    // first ~20 batches fill a fraction of the GPU and cost a wave's latency
+    // each): a 125k-row shard (the 8-GPU layout of C2) 0.138 -> 0.122 s, C2 1M
+    // 0.595 -> 0.585 s, recall unchanged (profiles/r03_build_probe.jsonl).
+    const double frac_early = env_double("VSG_BUILD_BATCH_FRAC", 2.0);
+    const double frac = env_double("VSG_BUILD_BATCH_FRAC2", 0.5);
+    const double switch_at = env_double("VSG_BUILD_BATCH_SWITCH", 8192);
     const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 65536);
     // at least 8 batches per call, so the call's own nodes find each other
-    const size_t bcall = std::max<size_t>(1, n / 8);
+    const size_t bcall = std::max<size_t>(1, n / std::max<size_t>(1, (size_t)env_double("VSG_BUILD_MIN_BATCHES", 8)));
     std::vector<uint32_t> pair_off(n);
     // split insert (launch_insert_split): the efC beam at its own occupancy, then
     // the selection; lists of (node, level) in HBM between the two (VSG_BUILD_SPLIT=0:
@@ -847,7 +884,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         while (i < n) {
             const size_t graph_nodes = (size_t)h->slots - n + i;
             size_t b = (size_t)std::floor((double)graph_nodes *
-                                          (switch_at > 0 && graph_nodes >= switch_at ? frac2 : frac));
+                                          (graph_nodes >= switch_at ? frac : frac_early));
             b = std::max<size_t>(1, std::min(std::min(b, bmax), bcall));
             b = std::min(b, n - i);
             int new_top = -1;
@@ -901,7 +938,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
             h->sort_tmp_bytes = tmp * 2;
         }
     }
-    while (h->ev_pool.size() < 4 * plan.size()) {  // device time of every launch
+    while (h->ev_pool.size() < 5 * plan.size()) {  // device time of every launch
         hipEvent_t x;
         HIP_TRY(hipEventCreate(&x));
         h->ev_pool.push_back(x);
@@ -923,10 +960,11 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     const int hash = hash_size_for(h->efc, (int)env_double("VSG_BUILD_HASH_FACTOR", h->row_bytes >= 1024 ? 16 : 8));
     for (size_t bi = 0; bi < plan.size(); ++bi) {
         const Batch& B = plan[bi];
-        hipEvent_t* ev = &h->ev_pool[4 * bi];
+        // ev: insert start | insert end | sort end | reverse end | beam end (split)
+        hipEvent_t* ev = &h->ev_pool[5 * bi];
         HIP_TRY(hipMemsetAsync(h->d_pk[0], 0xFF, B.npairs * 8, st));
         InsertParams ip{};
-        ip.g = h->graph();
+        ip.g = h->graph(edge_dist);
         ip.nodes = h->d_bnodes + B.i;
         ip.nnodes = (int)B.b;
         ip.levels = h->d_blevels + B.i;
@@ -950,7 +988,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
             ip.lst_d = h->d_lst_d;
             ip.lst_i = h->d_lst_i;
             ip.lst_n = h->d_lst_n;
-            HIP_TRY(launch_insert_split(h->st, h->mk, ip, st));
+            HIP_TRY(launch_insert_split(h->st, h->mk, ip, st, ev[4]));
         } else {
             HIP_TRY(launch_insert(h->st, h->mk, ip, st));
         }
@@ -959,7 +997,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         HIP_TRY(sort_pairs(h->d_sort_tmp, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], B.npairs, st));
         HIP_TRY(hipEventRecord(ev[2], st));
         ReverseParams rp{};
-        rp.g = h->graph();
+        rp.g = h->graph(edge_dist);
         rp.keys = h->d_pk[1];
         rp.vals = h->d_pv[1];
         rp.npairs = B.npairs;
@@ -981,13 +1019,20 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     if (!plan.empty()) {
         HIP_TRY(hipStreamSynchronize(st));
         pc.mark("b:device_drain");
+        // VSG_DEBUG_TIMING=2: one line per batch (probes)
+        const bool per_batch = env_double("VSG_DEBUG_TIMING", 0) >= 2;
         for (size_t bi = 0; bi < plan.size(); ++bi) {
-            float t[3] = {0.f, 0.f, 0.f};
+            float t[3] = {0.f, 0.f, 0.f}, tsel = 0.f;
             for (int j = 0; j < 3; ++j)
-                HIP_TRY(hipEventElapsedTime(&t[j], h->ev_pool[4 * bi + j], h->ev_pool[4 * bi + j + 1]));
+                HIP_TRY(hipEventElapsedTime(&t[j], h->ev_pool[5 * bi + j], h->ev_pool[5 * bi + j + 1]));
+            if (split) HIP_TRY(hipEventElapsedTime(&tsel, h->ev_pool[5 * bi + 4], h->ev_pool[5 * bi + 1]));
             h->t_insert_ns += (uint64_t)(t[0] * 1e6);
+            h->t_select_ns += (uint64_t)(tsel * 1e6);
             h->t_sort_ns += (uint64_t)(t[1] * 1e6);
             h->t_reverse_ns += (uint64_t)(t[2] * 1e6);
+            if (per_batch)
+                fprintf(stderr, "[vsg batch] %zu nodes=%zu graph=%zu pairs=%zu insert=%.3f select=%.3f sort=%.3f reverse=%.3f ms\n",
+                        bi, plan[bi].b, (size_t)s0 + plan[bi].i, plan[bi].npairs, t[0], tsel, t[1], t[2]);
         }
     }
     return VSG_OK;
@@ -1802,6 +1847,7 @@ int vsg_index_stats(const vsg_index_t* h, vsg_stats_t* out) {
     out->build_insert_ns = h->t_insert_ns;
     out->build_sort_ns = h->t_sort_ns;
     out->build_reverse_ns = h->t_reverse_ns;
+    out->build_select_ns = h->t_select_ns;
     return VSG_OK;
 }
 
@@ -1821,6 +1867,7 @@ int vsg_index_reset_stats(vsg_index_t* h) {
     h->build_vectors = 0;
     h->build_batches = 0;
     h->t_insert_ns = 0;
+    h->t_select_ns = 0;
     h->t_sort_ns = 0;
     h->t_reverse_ns = 0;
     return VSG_OK;
@@ -1922,6 +1969,7 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
         }
     h->entry = entry;
     h->max_level = max_level;
+    h->adjd_valid = false;  // filled by the next add (build_slots)
     publish(h);
     return VSG_OK;
 }
@@ -2237,6 +2285,7 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
     h->upper_used = fh.upper_rows;
     h->entry = fh.entry;
     h->max_level = fh.max_level;
+    h->adjd_valid = false;  // not in the file: filled by the next add
     h->live = 0;
     h->keys.reserve(fh.live);
     for (size_t i = 0; i < s; ++i)

@@ -17,6 +17,10 @@ struct DevGraph {
     const uint32_t* upper_off;
     uint32_t* upper;
     int M, M0;
+    // per-edge distances beside the adjacency (build only; nullptr in searches):
+    // adjd0[s * M0 + j] = dist(s, adj0[s * M0 + j]), upperd likewise for upper rows
+    float* adjd0;
+    float* upperd;
 };
 
 struct SearchParams {
@@ -152,9 +156,13 @@ hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipSt
 hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
 size_t search_reg_lds_bytes(int hash);
 // split insert: beam kernel then selection kernel (efc <= 192: register beam)
-hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s);
+hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s,
+                               hipEvent_t mid = nullptr);  // recorded between the two kernels
 hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s);
 hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int grid, hipStream_t s);
+// per-edge distances of slots [0, n) of an imported / loaded graph (levels: per slot)
+hipError_t launch_edge_dist_fill(Storage st, MetricKind mk, const DevGraph& g, const int8_t* levels, size_t n,
+                                 hipStream_t s);
 hipError_t launch_exact(Storage st, MetricKind mk, const ExactParams& p, hipStream_t s);
 hipError_t launch_merge_parts(const MergeParams& p, hipStream_t s);
 hipError_t launch_rerank(MetricKind mk, const RerankParams& p, hipStream_t s);
@@ -185,6 +193,7 @@ hipError_t launch_nearest_part(const float* part_d, const uint32_t* part_i, int 
 // okey[b] = cell[nodes[b] - s0] << 32 | b, oidx[b] = b for the n nodes of one batch
 hipError_t launch_batch_keys(const uint32_t* nodes, int n, uint32_t s0, const uint32_t* cell, uint64_t* okey,
                              uint32_t* oidx, hipStream_t s);
+
 hipError_t launch_datagen(int kind, size_t n, size_t dim, uint64_t seed, uint64_t model_seed,
                           size_t start_row, float* out, float* scratch_w, float* scratch_c,
                           hipStream_t s);

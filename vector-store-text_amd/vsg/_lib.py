@@ -68,6 +68,7 @@ class Stats(C.Structure):
         ("build_insert_ns", C.c_uint64),
         ("build_sort_ns", C.c_uint64),
         ("build_reverse_ns", C.c_uint64),
+        ("build_select_ns", C.c_uint64),
     ]
 
 

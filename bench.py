@@ -61,7 +61,10 @@ def parse():
     ap.add_argument("--config-ef", type=int, default=128,
                     help="also time the config's nominal efSearch (BASELINE configs[1]: 128); 0 = skip")
     ap.add_argument("--config", type=int, default=1, help="seed set (BASELINE.json configs index)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU-baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU search-baseline sample")
+    ap.add_argument("--cpu-build-rows", type=int, default=0,
+                    help="rows of the CPU build baseline (0 = all --rows: BASELINE.md's build vectors/s is "
+                         "N over the wall-clock insert time of the whole index)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--upper-ef", type=int, default=8,
                     help="N=1: also time the opt-in multi-entry descent at this level-1 beam width (0 = off)")
@@ -511,18 +514,28 @@ def run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_ove
     kms = kern_ms / a.steps
     flops = 2.0 * a.batch * nloc * a.dim
     tflops = flops / (kms * 1e-3) / 1e12
+    # batches below the MFMA tile threshold run the VALU kernel (vsg_index.cpp
+    # VSG_EXACT_MFMA_MIN = 32): HBM-bound, the whole base read once per launch
+    mfma = a.batch >= 32 and a.quant == "f32"
+    hbm_bytes = nloc * a.dim * (4 if a.quant == "f32" else 2) + a.batch * a.dim * 4
+    hbm_gbs = hbm_bytes / (kms * 1e-3) / 1e9
     out = {
-        "metric": f"brute-force kNN QPS (exact, f32 MFMA), {a.rows} x {a.dim} f32 {a.metric}, batch {a.batch}",
+        "metric": f"brute-force kNN QPS (exact, {'f32 MFMA' if mfma else 'VALU'}), {a.rows} x {a.dim} {a.quant} "
+                  f"{a.metric}, batch {a.batch}",
         "value": round(qps, 1), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(1000 * elapsed / a.steps, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py)",
         "config": {"workload": f"C5: {a.rows} x {a.dim} f32 {a.metric} brute force, k={a.k}",
                    "batch": a.batch, "parallelism": f"row-shard x{world}"},
-        "roofline": {"bound": "mfma", "achieved": round(tflops, 2), "peak": MFMA_F32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(tflops / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
-                     "kernel": "mfma_exact_kernel<16,MET> (+prepare, merge)", "kernel_ms": round(kms, 3),
-                     "flops_per_launch": flops},
+        "roofline": ({"bound": "mfma", "achieved": round(tflops, 2), "peak": MFMA_F32_PEAK_TFLOPS,
+                      "unit": "TFLOP/s", "frac": round(tflops / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                      "kernel": "mfma_exact_kernel<16,MET> (+prepare, merge)", "kernel_ms": round(kms, 3),
+                      "flops_per_launch": flops} if mfma else
+                     {"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(hbm_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                      "kernel": "exact_kernel (VALU, + prepare, merge)", "kernel_ms": round(kms, 3),
+                      "alg_bytes_per_launch": hbm_bytes, "tflops": round(tflops, 3)}),
     }
     if world == 1 and rank == 0 and not a.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -552,40 +565,58 @@ def run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_ove
 
 def build_roofline(a, head):
     """The build against the HBM roofline on DEVICE time (HIP events around every
-    batch's launches on the build stream, vsg_stats_t.build_*_ns), dominant kernel
-    hnsw_insert_kernel.  Algorithmic bytes of the insert kernel: one row per distance
-    evaluation of the descent and efC beam (distinct nodes of one wave's traversal) +
-    one level-0 adjacency row per expansion.  The heuristic selection's distances are
-    NOT counted: they re-score rows the beam just fetched (the kept set, <= M0 rows,
-    L1/L2-resident), so counting them credited cache hits as HBM bytes (round 1's
-    wall-time model reported 1.04 of peak at C3).  `traffic` = PMC HBM bytes of all
-    insert launches of the build (profiles/build_pmc.json, FETCH_SIZE x2 + WRITE_SIZE)
-    when it matches this workload."""
+    batch's launches on the build stream, vsg_stats_t.build_*_ns).  Dominant kernel:
+    hnsw_insert_beam_kernel (descent + efC beam; build_insert_ns - build_select_ns).
+    Algorithmic bytes per inserted vector: one row per distance evaluation of the
+    descent and beam (distinct nodes of one wave's traversal) + one level-0
+    adjacency row (M0 x 4 B) per expansion.  Beside it, each with its own line:
+      * hnsw_insert_select_kernel (heuristic neighbour selection): one row per
+        selection distance evaluation -- rows the beam fetched moments before, so
+        mostly L2 / MALL hits (achieved above HBM peak means cache hits);
+      * hnsw_reverse_kernel: one row per distance evaluation of the re-selection
+        (and of recomputed neighbour distances, zero since round 3 stores them
+        beside the adjacency).
+    `traffic` = PMC HBM bytes of the same kernel over the whole build
+    (profiles/build_pmc.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes) when it
+    matches this workload."""
     st, rb = head["bstats"], head["row_bytes"]
-    sel = st["build_select_distances"] + st["reverse_select_distances"] + st["reverse_recompute_distances"]
-    beam = st["build_distances"] - sel
-    ins_bytes = beam * rb + st["build_adjacency"] * 2 * a.M * 4
-    rev_bytes = st["reverse_recompute_distances"] * rb
-    t_ins, t_sort, t_rev = (max(1, st[f"build_{k}_ns"]) * 1e-9 for k in ("insert", "sort", "reverse"))
-    ach = ins_bytes / t_ins / 1e9
-    traffic = None
+    sel_ins = st["build_select_distances"]
+    sel_rev = st["reverse_select_distances"] + st["reverse_recompute_distances"]
+    beam = st["build_distances"] - sel_ins - sel_rev
+    beam_bytes = beam * rb + st["build_adjacency"] * 2 * a.M * 4
+    sel_bytes = sel_ins * rb
+    rev_bytes = sel_rev * rb
+    ns = {k: max(1, st[f"build_{k}_ns"]) * 1e-9 for k in ("insert", "sort", "reverse", "select")}
+    t_beam = max(1e-9, ns["insert"] - (ns["select"] if st["build_select_ns"] else 0.0))
+    pmc = {}
     try:
         d = json.load(open(os.path.join(ROOT, "profiles", "build_pmc.json")))
         w = d.get("workload", {})
         if (w.get("n"), w.get("dim"), w.get("metric"), w.get("M"), w.get("efc")) == (
                 head["nloc"], a.dim, a.metric, a.M, a.efc):
-            traffic = d.get("insert_hbm_bytes")
+            pmc = d
     except (OSError, ValueError):
         pass
-    return {"bound": "hbm", "kernel": "hnsw_insert_kernel", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "traffic_unit": "HBM bytes over all insert launches of the build",
-            "alg_bytes_insert": int(ins_bytes),
-            "kernel_s": {"insert": round(t_ins, 4), "sort": round(t_sort, 4), "reverse": round(t_rev, 4)},
-            "reverse_achieved_gbs": round(rev_bytes / t_rev / 1e9, 1),
+
+    def line(kernel, alg, t, traffic):
+        g = alg / t / 1e9
+        return {"kernel": kernel, "alg_bytes": int(alg), "kernel_s": round(t, 4), "achieved": round(g, 1),
+                "frac": round(g / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_over_alg": round(traffic / alg, 3) if traffic and alg else None}
+
+    ach = beam_bytes / t_beam / 1e9
+    return {"bound": "hbm", "kernel": "hnsw_insert_beam_kernel", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc.get("beam_hbm_bytes"),
+            "traffic_unit": "HBM bytes over all launches of the kernel in the build",
+            "alg_bytes_insert": int(beam_bytes),
+            "kernel_s": {"beam": round(t_beam, 4), "select": round(ns["select"], 4), "sort": round(ns["sort"], 4),
+                         "reverse": round(ns["reverse"], 4)},
+            "select": line("hnsw_insert_select_kernel", sel_bytes, ns["select"], pmc.get("select_hbm_bytes")),
+            "reverse": line("hnsw_reverse_kernel", rev_bytes, ns["reverse"], pmc.get("reverse_hbm_bytes")),
             "wall_s": round(head["build_s"], 4),
             "beam_distance_evals_per_vector": round(beam / max(1, head["nloc"]), 1),
-            "selection_distance_evals_per_vector": round(sel / max(1, head["nloc"]), 1)}
+            "selection_distance_evals_per_vector": round(sel_ins / max(1, head["nloc"]), 1),
+            "reverse_distance_evals_per_vector": round(sel_rev / max(1, head["nloc"]), 1)}
 
 
 def pmc_traffic(a, ef):
@@ -664,24 +695,23 @@ def cpu_baseline(a, index, q_t, ef, x_t, gt):
     res["recall_at_10"] = round(float(np.mean([len(set(ck[i].astype(np.int64)) & set(gt[i])) / a.k for i in range(ng)])), 4)
     res["ef"] = ef
     del h
-    # (2) build vectors/s: concurrent inserts into a fresh index, bounded sample
-    xh = x_t[: 200_000].cpu().numpy()
+    # (2) build vectors/s: the whole index (N / wall-clock insert time;
+    # the insert rate falls as the graph grows, so a prefix sample flatters it),
+    # concurrent one-vector inserts into a fresh index as the reference's rayon adds
+    nb = a.cpu_build_rows or a.rows
+    xh = x_t[:nb].cpu().numpy()
     hb = O.HnswOracle(a.dim, a.metric, a.M, a.efc, ef)
-    nb = 20_000
+    hb.reserve(nb)
     t0 = time.perf_counter()
-    hb.add(np.arange(nb), xh[:nb], threads=threads)
+    hb.add(np.arange(nb), xh, threads=threads)
     dt = time.perf_counter() - t0
-    nb2 = int(min(len(xh), max(nb, nb * (1 + a.cpu_seconds / max(dt, 1e-6)))))
-    hb2 = O.HnswOracle(a.dim, a.metric, a.M, a.efc, ef)
-    t0 = time.perf_counter()
-    hb2.add(np.arange(nb2), xh[:nb2], threads=threads)
-    dt = time.perf_counter() - t0
-    res["build_vectors_per_s"] = round(nb2 / dt, 1)
-    res["build_sample_rows"] = nb2
+    del hb, xh
+    res["build_vectors_per_s"] = round(nb / dt, 1)
+    res["build_seconds"] = round(dt, 2)
+    res["build_sample_rows"] = nb
     res["sample"] = (f"search: {n2} queries at ef={ef} over the GPU-built {a.rows}-row graph exported to host "
-                     f"(recall on the first {ng}); build: {nb2} inserts into a fresh index (efC={a.efc}, "
-                     f"M={a.M}) -- a bounded sample, not the full {a.rows} rows; {threads} threads, "
-                     f"{O.fast_isa()} f32 metrics")
+                     f"(recall on the first {ng}); build: all {nb} rows inserted into a fresh index "
+                     f"(efC={a.efc}, M={a.M}) in {dt:.1f} s; {threads} threads, {O.fast_isa()} f32 metrics")
     return res
 
 

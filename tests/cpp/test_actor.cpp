@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <map>
+#include <mutex>
 #include <random>
 #include <shared_mutex>
 #include <thread>
@@ -248,6 +249,45 @@ static void test_add_errors_swallowed() {
     CHECK(a.counters().add_errors == 1);
 }
 
+// 4b) add completions (vsg_actor_add_or_replace_cb): every add reports the status
+//     of the batched add that carried it, on the worker, once -- the host shim's
+//     BiMap rollback of a failed add (src/index/usearch.rs:230-232)
+struct DoneLog {
+    std::mutex m;
+    std::map<uint64_t, int> status;
+    int calls = 0;
+};
+static void on_done(void* ctx, uint64_t key, int st) {
+    auto* d = static_cast<DoneLog*>(ctx);
+    std::lock_guard<std::mutex> lk(d->m);
+    d->status[key] = st;
+    d->calls++;
+}
+
+static void test_add_completions() {
+    std::vector<Call> log;
+    std::vector<size_t> res;
+    auto* m = new Mock(2, 4, &log, &res, 0);
+    Mock* mp = m;
+    vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), vsg::ActorConfig{});
+    CHECK(a.init() == 0);
+    DoneLog d;
+    float v[2] = {1, 2};
+    for (uint64_t k = 0; k < 5; ++k) a.add_or_replace(k, v, on_done, &d);
+    CHECK(a.flush() == 0);
+    mp->fail_add = true;
+    a.add_or_replace(7, v, on_done, &d);
+    a.add_or_replace(3, v, on_done, &d);  // a replace whose add fails
+    CHECK(a.flush() == 0);
+    mp->fail_add = false;
+    a.add_or_replace(9, v);  // no completion requested
+    CHECK(a.flush() == 0);
+    CHECK(d.calls == 7);
+    for (uint64_t k = 0; k < 5; ++k) CHECK(d.status[k] == (k == 3 ? 4 : 0));
+    CHECK(d.status[7] == 4);
+    CHECK(a.size_now() == 5);  // 0,1,2,4 and 9; 3's old row was removed by the replace
+}
+
 // 5) tombstones (removes, and the old row of every replace) trigger a
 //    compaction once they reach compact_percent of the stored rows
 struct TombMock final : vsg::ActorBackend {
@@ -412,6 +452,7 @@ int main() {
     test_concurrent_anns();
     test_ef_groups_and_errors();
     test_add_errors_swallowed();
+    test_add_completions();
     test_auto_compaction();
     std::printf("ok\n");
     return 0;

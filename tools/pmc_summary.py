@@ -67,8 +67,9 @@ def build(fdir, wdir, n, dim, metric, M, efc, path=None):
            "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes; summed over every "
                          "dispatch of the kernel in ONE build (the probe builds once per process)"}
     # "hnsw_insert_": the fused insert kernel or both launches of the split insert
-    # (hnsw_insert_beam_kernel + hnsw_insert_select_kernel)
-    for tag, kern in (("insert", "hnsw_insert_"), ("reverse", "hnsw_reverse_kernel")):
+    # (hnsw_insert_beam_kernel + hnsw_insert_select_kernel), then each on its own
+    for tag, kern in (("insert", "hnsw_insert_"), ("beam", "hnsw_insert_beam_kernel"),
+                      ("select", "hnsw_insert_select_kernel"), ("reverse", "hnsw_reverse_kernel")):
         fv, _ = per_dispatch(fdir, "FETCH_SIZE", kern)
         wv, _ = per_dispatch(wdir, "WRITE_SIZE", kern)
         out[f"{tag}_dispatches"] = len(fv)

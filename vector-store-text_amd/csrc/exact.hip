@@ -94,6 +94,14 @@ __global__ __launch_bounds__(64) void merge_parts_kernel(MergeParams p) {
         const float cd = valid ? pd[i] : 0.f;
         L.merge(valid, cd, id, false, sd, si);
     }
+    if (p.out_part_d) {  // stage 1 of a two-stage merge: a partial list again
+        for (int j = lane; j < p.k; j += 64) {
+            const bool v = j < L.size;
+            p.out_part_d[(size_t)qi * p.k + j] = v ? L.D()[j] : __builtin_inff();
+            p.out_part_i[(size_t)qi * p.k + j] = v ? (L.I()[j] & VSG_ID_MASK) : VSG_EMPTY;
+        }
+        return;
+    }
     uint64_t* ok = p.out_keys + (size_t)qi * p.k;
     float* od = p.out_dist + (size_t)qi * p.k;
     for (int j = lane; j < p.k; j += 64) {

@@ -29,7 +29,12 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int KT = 32;   // dims per stage = one 128-B LDS row
 constexpr int LDK = 32;  // LDS row stride (floats), unpadded: glds writes lane-linear 1-KiB pieces
-constexpr int STAGE_FLOATS = (MFMA_BR + MFMA_BQ) * LDK;
+// WQ = waves along the query axis: 2 -> 128 rows x 128 queries, 256 threads;
+// 1 -> 128 rows x 64 queries, 128 threads (batches of <= 64 queries: the 128-query
+// tile computed half of its MFMAs for clamped padding queries, 0.28 of peak at 64)
+template <int WQ> struct MfmaTile {
+    static constexpr int BQ = 64 * WQ, NW = 2 * WQ, STAGE = (MFMA_BR + BQ) * LDK;
+};
 
 // 16-B slot of logical chunk c (0..7) in LDS row R: XOR swizzle so the sixteen
 // lanes of a ds_read_b128 group (rows R..R+15, same chunk) hit distinct slots of
@@ -55,14 +60,16 @@ __device__ __forceinline__ void topk_insert(float (&ld)[KMAX], uint32_t (&li)[KM
     }
 }
 
-template <int KMAX, int MET>
-__global__ __launch_bounds__(256, 2) void mfma_exact_kernel(MfmaExactParams p) {
-    __shared__ __attribute__((aligned(16))) float lds_a[STAGE_FLOATS];
-    __shared__ __attribute__((aligned(16))) float lds_b[STAGE_FLOATS];
+template <int KMAX, int MET, int WQ>
+__global__ __launch_bounds__(128 * WQ, 2) void mfma_exact_kernel(MfmaExactParams p) {
+    using TL = MfmaTile<WQ>;
+    constexpr int BQ = TL::BQ, NW = TL::NW;
+    __shared__ __attribute__((aligned(16))) float lds_a[TL::STAGE];
+    __shared__ __attribute__((aligned(16))) float lds_b[TL::STAGE];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int w = tid >> 6;
-    const int wq = w & 1, wr = w >> 1;
+    const int wq = WQ == 2 ? (w & 1) : 0, wr = WQ == 2 ? (w >> 1) : w;
     const int h = lane >> 5, r = lane & 31;
 
     // XCD-contiguous block -> (split, query tile)
@@ -72,7 +79,7 @@ __global__ __launch_bounds__(256, 2) void mfma_exact_kernel(MfmaExactParams p) {
     if (L >= p.qtiles * p.splits) return;
     const int split = L / p.qtiles;
     const int qt = L % p.qtiles;
-    const int q0 = qt * MFMA_BQ;
+    const int q0 = qt * BQ;
     const size_t ntiles = (p.nslots + MFMA_BR - 1) / MFMA_BR;
     const size_t t_beg = (size_t)split * p.tiles_per_split;
     const size_t t_end = min(t_beg + (size_t)p.tiles_per_split, ntiles);
@@ -107,24 +114,34 @@ __global__ __launch_bounds__(256, 2) void mfma_exact_kernel(MfmaExactParams p) {
 #pragma unroll
                 for (int g = 0; g < 16; ++g) acc[a][b][g] = 0.f;
 
-        // LDS-DMA staging: wave w fills 1-KiB pieces w*4+u (8 rows x 128 B) of the
-        // base-row and query tiles; out-of-range rows read a clamped valid row
-        // (masked in the epilogue / never written out).
+        // LDS-DMA staging: the NW waves fill the 1-KiB pieces (8 rows x 128 B) of the
+        // base-row tile (16 pieces) and the query tile (BQ / 8 pieces) round-robin;
+        // out-of-range rows read a clamped valid row (masked in the epilogue / never
+        // written out).
         const int prow = lane >> 3, pslot = lane & 7;
+        // Addresses: a wave-uniform stage base + a 32-bit per-lane offset (row within
+        // the tile, clamped, x row_floats + swizzled chunk), so no 64-bit address per
+        // piece stays live across the K loop (the 64-query tile spilled with them).
+        const int xlast = (int)min((size_t)(MFMA_BR - 1), p.nslots - 1 - r0);
+        const int qlast = min(BQ - 1, p.nq - 1 - q0);
         auto load_stage = [&](int s, float* xs) {
             const int k0 = s * KT;
             float* qs = xs + MFMA_BR * LDK;
+            const float* xb = p.vecs + r0 * p.row_floats + k0;
+            const float* qb = p.queries + (size_t)q0 * p.row_floats + k0;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int piece = w * 4 + u;
+            for (int u = 0; u < MFMA_BR / 8 / NW; ++u) {
+                const int piece = w * (MFMA_BR / 8 / NW) + u;
                 const int R = piece * 8 + prow;
-                const int c = swz(R, pslot);
-                const size_t grow = min(r0 + (size_t)R, p.nslots - 1);
-                const size_t gq = (size_t)min(q0 + R, p.nq - 1);
-                __builtin_amdgcn_global_load_lds((gptr_t)(p.vecs + grow * p.row_floats + k0 + c * 4),
-                                                 (lptr_t)(xs + piece * 8 * LDK), 16, 0, 0);
-                __builtin_amdgcn_global_load_lds((gptr_t)(p.queries + gq * p.row_floats + k0 + c * 4),
-                                                 (lptr_t)(qs + piece * 8 * LDK), 16, 0, 0);
+                const uint32_t off = (uint32_t)min(R, xlast) * (uint32_t)p.row_floats + (uint32_t)swz(R, pslot) * 4;
+                __builtin_amdgcn_global_load_lds((gptr_t)(xb + off), (lptr_t)(xs + piece * 8 * LDK), 16, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < BQ / 8 / NW; ++u) {
+                const int piece = w * (BQ / 8 / NW) + u;
+                const int R = piece * 8 + prow;
+                const uint32_t off = (uint32_t)min(R, qlast) * (uint32_t)p.row_floats + (uint32_t)swz(R, pslot) * 4;
+                __builtin_amdgcn_global_load_lds((gptr_t)(qb + off), (lptr_t)(qs + piece * 8 * LDK), 16, 0, 0);
             }
         };
         // one K stage: MFMAs on `cur` while the next stage streams into `nxt`.
@@ -207,11 +224,16 @@ __global__ __launch_bounds__(256, 2) void mfma_exact_kernel(MfmaExactParams p) {
 }
 
 hipError_t launch_mfma_exact(MetricKind mk, const MfmaExactParams& p, hipStream_t s) {
-    if (p.kmax != 16) return hipErrorNotSupported;
+    if (p.kmax != 16 || (p.bq != 64 && p.bq != 128)) return hipErrorNotSupported;
     const int total = p.qtiles * p.splits;
     const int nb = (total + 7) / 8 * 8;
-    auto kern = mk == MK_L2 ? mfma_exact_kernel<16, MET_L2> : mfma_exact_kernel<16, MET_DOT>;
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, p);
+    if (p.bq == 128) {
+        auto kern = mk == MK_L2 ? mfma_exact_kernel<16, MET_L2, 2> : mfma_exact_kernel<16, MET_DOT, 2>;
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, p);
+    } else {
+        auto kern = mk == MK_L2 ? mfma_exact_kernel<16, MET_L2, 1> : mfma_exact_kernel<16, MET_DOT, 1>;
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(128), 0, s, p);
+    }
     return hipGetLastError();
 }
 

@@ -698,6 +698,7 @@ static hipError_t rows_to_cells(vsg_index* h, const uint8_t* rows, const float* 
     mp.splits = cs.splits;
     mp.tiles_per_split = cs.tps;
     mp.kmax = 16;
+    mp.bq = MFMA_BQ;
     mp.part_d = part_d;
     mp.part_i = part_i;
     hipError_t e = launch_mfma_exact(h->mk, mp, st);
@@ -1477,10 +1478,11 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
                           nq >= mfma_min && h->pub_slots > 0 && env_double("VSG_EXACT_MFMA", 1) != 0;
     // plan: partial-list shapes, then one scratch block for everything
     const size_t slots = h->pub_slots;  // rows of the last completed add
-    int qtiles = 0, kmax = 0, nparts = 0, nblocks = 1, rpb = 1;
-    size_t splits = 0, tps = 0, np = 0;
+    int qtiles = 0, kmax = 0, nparts = 0, nblocks = 1, rpb = 1, ngroups = 0;
+    size_t splits = 0, tps = 0, np = 0, np_lists = 0;
+    const int bq = nq <= 64 ? 64 : MFMA_BQ;  // the 64-query tile for small batches
     if (use_mfma) {
-        qtiles = (int)((nq + MFMA_BQ - 1) / MFMA_BQ);
+        qtiles = (int)((nq + bq - 1) / bq);
         const size_t ntiles = (slots + MFMA_BR - 1) / MFMA_BR;
         splits = std::min<size_t>(ntiles, std::max<size_t>(1, (1024 + qtiles - 1) / qtiles));
         tps = (ntiles + splits - 1) / splits;
@@ -1489,14 +1491,27 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         nparts = (int)splits * 4;
         np = nq * (size_t)nparts * kmax;
     } else if (exact) {
-        // grid.y = row blocks (<= 65535 per dimension)
-        nblocks = (int)std::min<size_t>(32768, std::max<size_t>(1, (slots + 4095) / 4096));
+        // grid.y = row blocks (<= 65535 per dimension).  4,096-row blocks fill the
+        // chip from ~32 queries on; a smaller batch gets more, shorter blocks so
+        // the launch still holds >= VSG_EXACT_MIN_WAVES waves (at one query the
+        // 245 waves of 4,096-row blocks read C5's 6 GB at 0.11 of HBM,
+        // profiles/r03_bench_c5_batches.jsonl), down to 64 rows per block
+        const size_t want = (size_t)env_double("VSG_EXACT_MIN_WAVES", 8192);
+        size_t nb = std::max<size_t>((slots + 4095) / 4096, std::min((want + nq - 1) / nq, (slots + 63) / 64));
+        nblocks = (int)std::min<size_t>(32768, std::max<size_t>(1, nb));
         // large k: bound the partial lists (nq x nblocks x k x 8 B) to ~1 GiB
         const size_t cap_blocks = std::max<size_t>(1, ((size_t)1 << 30) / (8 * nq * k));
         nblocks = (int)std::min<size_t>((size_t)nblocks, cap_blocks);
+        // more than 64 lists per query: merged in two stages (64-list groups in
+        // parallel, then the group results), not by one wave walking all of them
+        if (nblocks > 64 && slots > 0) {
+            nblocks = (nblocks + 63) / 64 * 64;  // padding blocks hold no rows (empty lists)
+            ngroups = nblocks / 64;
+        }
         rpb = (int)((slots + nblocks - 1) / nblocks);
         if (slots == 0) nblocks = 1;
-        np = nq * (size_t)nblocks * k;
+        np_lists = nq * (size_t)nblocks * k;
+        np = np_lists + (ngroups ? nq * (size_t)ngroups * k : 0);
     }
     // f16 traversal: the beam (ef slots) of the f16 search is re-ranked in f32
     const bool rerank = !exact && h->f16_trav && slots > 0;
@@ -1537,6 +1552,7 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         mp.splits = (int)splits;
         mp.tiles_per_split = (int)tps;
         mp.kmax = kmax;
+        mp.bq = bq;
         mp.part_d = pd;
         mp.part_i = pi;
         err = launch_mfma_exact(h->mk, mp, s);
@@ -1636,12 +1652,23 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         ep.part_d = pd;
         ep.part_i = pi;
         err = slots > 0 ? launch_exact(h->st, h->mk, ep, s) : hipMemsetAsync(pi, 0xFF, np * 4, s);
+        if (err == hipSuccess && ngroups) {  // stage 1: each 64-list group -> one list
+            MergeParams g1{};
+            g1.part_d = pd;
+            g1.part_i = pi;
+            g1.nq = (int)(nq * ngroups);
+            g1.parts = 64;
+            g1.k = (int)k;
+            g1.out_part_d = pd + np_lists;
+            g1.out_part_i = pi + np_lists;
+            err = launch_merge_parts(g1, s);
+        }
         if (err == hipSuccess) {
             MergeParams mp{};
-            mp.part_d = pd;
-            mp.part_i = pi;
+            mp.part_d = ngroups ? pd + np_lists : pd;
+            mp.part_i = ngroups ? pi + np_lists : pi;
             mp.nq = (int)nq;
-            mp.parts = nblocks;
+            mp.parts = ngroups ? ngroups : nblocks;
             mp.k = (int)k;
             mp.keys = h->d_keys;
             mp.out_keys = ok;

@@ -104,6 +104,7 @@ struct MfmaExactParams {
     int qtiles, splits;
     int tiles_per_split;    // 128-row tiles per split
     int kmax;
+    int bq;                 // queries per tile: 128 (256-thread blocks) or 64 (batches <= 64)
     float* part_d;
     uint32_t* part_i;
 };
@@ -117,6 +118,10 @@ struct MergeParams {
     uint64_t* out_keys;
     float* out_dist;
     uint32_t* out_counts;
+    // set: write the merged list as (distance, slot) partial-list entries
+    // (nq x k, EMPTY padded) instead of keys -- stage 1 of a two-stage merge
+    float* out_part_d;
+    uint32_t* out_part_i;
 };
 
 // f16-traversal re-rank (rerank.hip): exact f32 distances of each query's

@@ -65,10 +65,13 @@ def main():
         for ef in (int(e) for e in a.efs.split(",")):
             f = idx.search_device(q, 10, ef)[0].cpu().numpy()
             rec[ef] = round(float((f[:, :, None] == gt[:, None, :]).any(axis=1).sum(axis=1).mean() / 10), 4)
-        line = {"rows": a.rows, "dim": a.dim, "setting": kv or "base", "wall_s": [round(w, 4) for w in walls],
+        line = {"rows": a.rows, "dim": a.dim, "setting": kv or "base",
+                "lib": os.environ.get("VSG_LIB_PATH", "lib/libvsg.so").split("/")[-2], "wall_s": [round(w, 4) for w in walls],
                 "insert_s": round(st["build_insert_ns"] * 1e-9, 4), "sort_s": round(st["build_sort_ns"] * 1e-9, 4),
                 "reverse_s": round(st["build_reverse_ns"] * 1e-9, 4),
                 "select_s": round(st["build_select_ns"] * 1e-9, 4), "batches": st["build_batches"],
+                "select_dist_per_vec": round(st["build_select_distances"] / a.rows, 1),
+                "reverse_dist_per_vec": round((st["reverse_select_distances"] + st["reverse_recompute_distances"]) / a.rows, 1),
                 "recall": rec, "vec_per_s": round(a.rows / min(walls), 1)}
         print(json.dumps(line), flush=True)
         with open(a.out, "a") as fo:

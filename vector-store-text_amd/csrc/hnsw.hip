@@ -138,10 +138,30 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
 #ifndef VSG_SEL_U_REVERSE
 #define VSG_SEL_U_REVERSE VSG_SEL_U
 #endif
-template <int G, int VM, int U, typename T, int MET, int SU = VSG_SEL_U>
+// Selection row shape (probes): VSG_SEL_G64 lays a 32-lane row shape with an even
+// VM over the whole wave (G 64, VM / 2: half the candidate image, so twice the
+// candidates per block at the same registers); VSG_SEL_NQMAX caps the block.
+#ifndef VSG_SEL_G64
+#define VSG_SEL_G64 0
+#endif
+#ifndef VSG_SEL_NQMAX
+#define VSG_SEL_NQMAX 4
+#endif
+template <int G, int VM> struct SelShape {
+    static constexpr bool W = VSG_SEL_G64 && G == 32 && VM % 2 == 0;
+    static constexpr int G2 = W ? 64 : G, VM2 = W ? VM / 2 : VM;
+};
+template <int QF> constexpr int sel_nq() {
+    int nq = VSG_SEL_NQMAX;
+    while (nq > 1 && nq * QF > VSG_SEL_VGPRS) --nq;
+    return nq;
+}
+
+template <int G0, int VM0, int U, typename T, int MET, int SU = VSG_SEL_U>
 __device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uint64_t& ndist) {
+    constexpr int G = SelShape<G0, VM0>::G2, VM = SelShape<G0, VM0>::VM2;
     constexpr int QF = VM * ChunkT<T>::E;
-    constexpr int NQ = QF * 4 <= VSG_SEL_VGPRS ? 4 : QF * 3 <= VSG_SEL_VGPRS ? 3 : QF * 2 <= VSG_SEL_VGPRS ? 2 : 1;
+    constexpr int NQ = sel_nq<QF>();
     constexpr int UT = SU;  // row passes in flight per test
     constexpr int BLK = (64 / G) * UT;
     const int lane = lane_id();

@@ -82,7 +82,7 @@ def parse():
                     help="experiment: insert base rows in synthetic-cluster order (spatial slot ids)")
     ap.add_argument("--multi", default="both", choices=("both", "shard", "replica"),
                     help="N>1: row-range shards + all-gather merge (strong) and/or full replicas + query "
-                         "split (weak); 'both' reports replica QPS as value and the shard leg beside it")
+                         "split (weak); 'both' reports the shard leg as value and the replica leg beside it")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse several ranks on one GPU (collectives via host)")
     return ap.parse_args()

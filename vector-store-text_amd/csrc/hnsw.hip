@@ -138,6 +138,11 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
 #ifndef VSG_SEL_U_REVERSE
 #define VSG_SEL_U_REVERSE VSG_SEL_U
 #endif
+// register rows of the build's efC beam (64 R >= efC + 64; more rows: fewer
+// compactions, more VGPRs)
+#ifndef VSG_BUILD_REG_R
+#define VSG_BUILD_REG_R 4
+#endif
 // Selection row shape (probes): VSG_SEL_G64 lays a 32-lane row shape with an even
 // VM over the whole wave (G 64, VM / 2: half the candidate image, so twice the
 // candidates per block at the same registers); VSG_SEL_NQMAX caps the block.
@@ -484,9 +489,9 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
         if (p.efc <= 192) {
             // candidate set in VGPRs (hnsw_regset.hpp), then the sorted top-efc
             // list the selection walks -- the list beam's exact result
-            RegSet<4> B;
-            beam_reg<G, VM, U, T, MET, 4>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf);
-            regset_to_list<4>(B, p.efc, w);
+            RegSet<VSG_BUILD_REG_R> B;
+            beam_reg<G, VM, U, T, MET, VSG_BUILD_REG_R>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf);
+            regset_to_list<VSG_BUILD_REG_R>(B, p.efc, w);
         } else {
             beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, pf);
         }
@@ -558,9 +563,9 @@ __global__ __launch_bounds__(64) void hnsw_insert_beam_kernel(InsertParams p) {
     ++ndist;
     for (int l = p.max_level; l > L; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
     for (int l = min(L, p.max_level); l >= 0; --l) {
-        RegSet<4> B;
-        beam_reg<G, VM, U, T, MET, 4>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf);
-        regset_to_list<4>(B, p.efc, w);
+        RegSet<VSG_BUILD_REG_R> B;
+        beam_reg<G, VM, U, T, MET, VSG_BUILD_REG_R>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf);
+        regset_to_list<VSG_BUILD_REG_R>(B, p.efc, w);
         const size_t slot = (size_t)p.list_off[bi] + (size_t)l;
         const int n = w.list.size;
         float* od = p.lst_d + slot * (size_t)p.efc;
@@ -629,6 +634,44 @@ __global__ __launch_bounds__(64) VSG_SEL_WAVES void hnsw_insert_select_kernel(In
 // segment heads; each segment (level, v) is merged into v's row: append while
 // there is room, else heuristic re-selection over existing + incoming.
 
+// Entries in use of an adjacency row (a compact prefix), read by one lane: 16 B
+// at a time when rows are 16-B aligned (m % 4 == 0), stopping at the first piece
+// that is not full.
+#ifndef VSG_REVERSE_LANE_APPEND
+#define VSG_REVERSE_LANE_APPEND 1
+#endif
+__device__ __forceinline__ int row_fill(const uint32_t* row, int m) {
+    int ne = 0;
+    if ((m & 3) == 0) {
+        const uint4* r4 = reinterpret_cast<const uint4*>(row);
+        const int m4 = m >> 2;
+        for (int c0 = 0; c0 < m4; c0 += 8) {
+            int cnt = 0;
+            uint4 x[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                x[j] = c0 + j < m4 ? r4[c0 + j] : make_uint4(VSG_EMPTY, VSG_EMPTY, VSG_EMPTY, VSG_EMPTY);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                cnt += (x[j].x != VSG_EMPTY) + (x[j].y != VSG_EMPTY) + (x[j].z != VSG_EMPTY) + (x[j].w != VSG_EMPTY);
+            ne += cnt;
+            if (cnt < 32) break;
+        }
+    } else {
+        for (int c0 = 0; c0 < m; c0 += 8) {
+            int cnt = 0;
+            uint32_t x[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = c0 + j < m ? row[c0 + j] : VSG_EMPTY;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cnt += x[j] != VSG_EMPTY;
+            ne += cnt;
+            if (cnt < 8) break;
+        }
+    }
+    return ne;
+}
+
 // One instance for both paths (stored distances / recomputed): compiled as two
 // instances, the stored-distance one got 185 VGPRs instead of 239 and ran 50 %
 // slower (C2 reverse 54 -> 82 ms; profiles/r03_build_probe.jsonl) -- the larger
@@ -652,6 +695,43 @@ __global__ __launch_bounds__(64) VSG_REV_WAVES void hnsw_reverse_kernel(ReverseP
         const uint64_t prev = (i < end && i > 0) ? p.keys[i - 1] : ~0ull;
         const bool head = key != ~0ull && (i == 0 || (key >> PAIR_V_SHIFT) != (prev >> PAIR_V_SHIFT));
         uint64_t heads = __ballot(head);
+        nadj += (uint64_t)popc64(heads);
+        if (VSG_REVERSE_LANE_APPEND) {
+            // Appends, one segment per head lane: each lane reads its own row's
+            // fill (one round trip for every segment of the window, where the
+            // wave-wide path below pays one per segment) and appends when the
+            // segment fits.  Segments touch only their own (level, v) row, so
+            // the order they are applied in changes nothing.
+            bool fits = false;
+            if (head) {
+                const uint64_t seg = key >> PAIR_V_SHIFT;
+                const int l = (int)(key >> PAIR_L_SHIFT);
+                const uint32_t v = (uint32_t)(seg & PAIR_ID_MASK);
+                const uint64_t above = heads & ~((2ull << lane) - 1ull);  // later heads of the window
+                size_t e;
+                if (above) {
+                    e = i0 + (size_t)__builtin_ctzll(above);
+                } else {  // the window's last segment: scan on (segments are short)
+                    e = i + 1;
+                    while (e < p.npairs && (p.keys[e] >> PAIR_V_SHIFT) == seg) ++e;
+                }
+                const int nin = (int)(e - i);
+                const int m = l == 0 ? g.M0 : g.M;
+                uint32_t* row = g.row(v, l);
+                const int ne = row_fill(row, m);
+                if (ne + nin <= m) {
+                    fits = true;
+                    float* rowd = g.adjd0 ? g.rowd(v, l) : nullptr;
+                    for (int t = 0; t < nin; ++t) {
+                        row[ne + t] = (uint32_t)(p.keys[i + t] & PAIR_ID_MASK);
+                        if (rowd) rowd[ne + t] = __uint_as_float(p.vals[i + t]);
+                    }
+                }
+            }
+            const uint64_t done = __ballot(fits);
+            nappend += (uint64_t)popc64(done);
+            heads &= ~done;  // the segments that need a prune
+        }
         while (heads) {
             const int hl = __builtin_ctzll(heads);
             heads &= heads - 1;
@@ -675,7 +755,6 @@ __global__ __launch_bounds__(64) VSG_REV_WAVES void hnsw_reverse_kernel(ReverseP
             const int nin = (int)(e - h);
             const int m = l == 0 ? g.M0 : g.M;
             uint32_t* row = g.row(v, l);
-            ++nadj;
             int ne = 0;  // rows are a compact prefix (M0 <= 128: up to two pieces)
             for (int c0 = 0; c0 < m; c0 += 64) {
                 const uint32_t x = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;

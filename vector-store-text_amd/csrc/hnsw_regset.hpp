@@ -8,6 +8,11 @@ namespace vsg {
 
 #define VSG_KEY_EMPTY (~0ull)
 
+// compaction may stop at a prefix range instead of the exact keep-th key (probes)
+#ifndef VSG_COMPACT_EARLY
+#define VSG_COMPACT_EARLY 0
+#endif
+
 // (distance, slot) -> key whose unsigned order is cand_less order (-0 == +0).
 __device__ __forceinline__ uint64_t cand_key(float d, uint32_t id) {
     uint32_t b = __float_as_uint(d);
@@ -92,6 +97,15 @@ template <int R> struct RegSet {
     __device__ __forceinline__ void compact(int keep) {
         uint32_t ph = 0;
         int need = keep;
+#if VSG_COMPACT_EARLY
+        // Any cut at or above the keep-th key keeps B a superset of the top
+        // `keep` (the traversal only needs that), so the select may stop at the
+        // first prefix range whose keys, with every key below it, fit in half
+        // the slack between `keep` and 64 (R - 1) (room for one more expansion):
+        // fewer ballot passes, and the next compaction is not much earlier.
+        int rsize = size;  // keys in the current prefix range (bits above b fixed)
+        const int cap = keep + (64 * (R - 1) - keep) / 2;
+#endif
 #pragma unroll 1
         for (int b = 31; b >= 0; --b) {
             const uint32_t hm = b == 31 ? 0u : (~0u << (b + 1));
@@ -104,7 +118,28 @@ template <int R> struct RegSet {
             if (c < need) {
                 need -= c;
                 ph |= 1u << b;
+#if VSG_COMPACT_EARLY
+                rsize -= c;
+#endif
             }
+#if VSG_COMPACT_EARLY
+            else {
+                rsize = c;
+            }
+            const int kept = keep - need + rsize;  // keys below the range + the range
+            if (b > 0 && kept <= cap) {
+                const uint64_t cut = ((uint64_t)(ph | ((1u << b) - 1u)) << 32) | 0xFFFFFFFFull;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (k[r] > cut) {
+                        k[r] = VSG_KEY_EMPTY;
+                        expm &= ~(1u << r);
+                    }
+                size = kept;
+                tkey = cut;
+                return;
+            }
+#endif
         }
         int ceq = 0;
 #pragma unroll

@@ -137,7 +137,13 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
     if (p.ef < 1 || p.ef > 1024 || p.k > p.ef || p.hash_size < p.k) return hipErrorInvalidValue;
     const size_t lds = search_reg_lds_bytes(p.hash_size);
     hipError_t err = hipSuccess;
-    const int rows = reg_rows(p.ef);
+    // VSG_SEARCH_REG_ROWS (probes): more register rows than the minimum --
+    // same results (B is any superset of the top ef), fewer compactions
+    int rows = reg_rows(p.ef);
+    if (const char* e = getenv("VSG_SEARCH_REG_ROWS")) {
+        const int r = atoi(e);
+        if ((r == 2 || r == 4 || r == 8 || r == 17) && 64 * r >= p.ef + 64) rows = r;
+    }
     dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
         using T = typename decltype(tt)::T;

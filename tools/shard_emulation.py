@@ -87,21 +87,31 @@ def main():
     for ef in [int(e) for e in a.efs.split(",")]:
         f_ = merged(qgt, ef)[0].cpu().numpy()
         rec = float(np.mean([len(set(f_[i]) & set(gt[i])) / a.k for i in range(gt.shape[0])]))
-        per = []
+        per, dpq, gbs = [], [], []
+        per16 = 4 if a.quant == "f32" else 8
+        row_bytes = (a.dim + per16 - 1) // per16 * 16
         for s in shards:
             s.search_device(q, a.k, ef)  # warm
+            s.reset_stats()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.steps):
                 s.search_device(q, a.k, ef)
             torch.cuda.synchronize()
             per.append((time.perf_counter() - t0) / a.steps)
+            st = s.stats()
+            nq = max(1, st["search_queries"])
+            # per-shard algorithmic bytes (rows evaluated + adjacency rows read)
+            alg = (st["search_distances"] * row_bytes + st["search_adjacency"] * 32 * 4) / a.steps
+            dpq.append(round(st["search_distances"] / nq, 1))
+            gbs.append(round(alg / per[-1] / 1e9, 1))
         tm = time.perf_counter()
         for _ in range(a.steps):
             merged(q, ef)
         torch.cuda.synchronize()
         t_all = (time.perf_counter() - tm) / a.steps
         line = {"ef": ef, "recall_at_10": round(rec, 4), "shard_ms": [round(1000 * p, 3) for p in per],
+                "dist_evals_per_query_per_shard": dpq, "alg_gbs_per_shard": gbs,
                 "qps_projected_gpus": round(a.queries / max(per), 1),
                 "qps_1gpu_all_shards": round(a.queries / t_all, 1)}
         with open(a.out, "a") as f:

@@ -30,18 +30,43 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int o) {
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
     return ((uint64_t)hi << 32) | lo;
 }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+template <int CTRL> __device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+// Wave minimum, result in every lane.  A minimum is exact in any order, so the
+// 16-lane rows reduce with DPP moves (quad xor 1 / 2, half-row and row mirrors:
+// every lane of a row then holds the row's minimum) and the four rows meet in
+// scalar registers -- no ds_bpermute round trips (12 of them in the xor
+// butterfly of two 32-bit halves).
 __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+#if VSG_DPP_REDUCE
+    uint64_t w;
+    w = dpp64<0xB1>(v);
+    v = w < v ? w : v;
+    w = dpp64<0x4E>(v);
+    v = w < v ? w : v;
+    w = dpp64<0x141>(v);
+    v = w < v ? w : v;
+    w = dpp64<0x140>(v);
+    v = w < v ? w : v;
+    const uint64_t r0 = readlane64(v, 0), r1 = readlane64(v, 16), r2 = readlane64(v, 32), r3 = readlane64(v, 48);
+    const uint64_t a = r0 < r1 ? r0 : r1, b = r2 < r3 ? r2 : r3;
+    return a < b ? a : b;
+#else
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const uint64_t w = shfl_xor64(v, o);
         v = w < v ? w : v;
     }
     return v;
-}
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-    return ((uint64_t)hi << 32) | lo;
+#endif
 }
 
 template <int R> struct RegSet {

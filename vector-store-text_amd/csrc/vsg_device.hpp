@@ -7,7 +7,7 @@
 // Base rows are fetched straight to VGPRs in 16-B chunks: a row is split over
 // G lanes (G in {4..64}), each lane holds VM chunks, 64/G rows per pass, U
 // passes issued back-to-back before any arithmetic so 8-16 loads per lane are
-// in flight; partial sums are reduced across the G lanes with xor shuffles.
+// in flight; partial sums are reduced across the G lanes (group_sum0: DPP adds).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -51,6 +51,31 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// Sum of `a` over each G-lane group, valid in the group's first lane only: the
+// value the xor butterfly (offsets G/2, ..., 2, 1) leaves there, bit for bit --
+// each step adds lane i + o to lane i for the lanes i < o that still feed lane 0,
+// with the same operands in the same order.  The steps inside a 16-lane row are
+// DPP modifiers of the adds (row_shl 8 / 4, quad_perm) instead of ds_bpermute
+// round trips through the LDS crossbar; 16 is a ds_swizzle (xor within 32
+// lanes), 32 one ds_bpermute.  Lanes other than the first hold partial sums.
+#ifndef VSG_DPP_REDUCE
+#define VSG_DPP_REDUCE 1
+#endif
+template <int G> __device__ __forceinline__ float group_sum0(float a) {
+#if VSG_DPP_REDUCE
+    if constexpr (G >= 64) a += __shfl_xor(a, 32);
+    if constexpr (G >= 32) a += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(a), 0x401F));
+    if constexpr (G >= 16) a += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), 0x108, 0xF, 0xF, true));
+    if constexpr (G >= 8) a += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), 0x104, 0xF, 0xF, true));
+    if constexpr (G >= 4) a += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), 0x4E, 0xF, 0xF, true));
+    if constexpr (G >= 2) a += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), 0xB1, 0xF, 0xF, true));
+#else
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) a += __shfl_xor(a, o);
+#endif
+    return a;
+}
+
 __device__ __forceinline__ bool cand_less(float da, uint32_t ia, float db, uint32_t ib) {
     return da < db || (da == db && ia < ib);
 }
@@ -69,8 +94,37 @@ template <typename X> __device__ __forceinline__ X readlane(X x, int l) {
     }
 }
 
-// Lexicographic (d, id) minimum across the wave; result in all lanes.
+// Lexicographic (d, id) minimum across the wave; result in all lanes.  Exact in
+// any order: DPP moves inside each 16-lane row (quad xor 1 / 2, half-row and row
+// mirrors), then the four row minima through scalar registers.
+template <int CTRL> __device__ __forceinline__ void argmin_dpp_step(float& d, uint32_t& id) {
+    const float od = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(d), CTRL, 0xF, 0xF, false));
+    const uint32_t oi = (uint32_t)__builtin_amdgcn_mov_dpp((int)id, CTRL, 0xF, 0xF, false);
+    if (cand_less(od, oi, d, id)) {
+        d = od;
+        id = oi;
+    }
+}
 __device__ __forceinline__ void wave_argmin(float& d, uint32_t& id) {
+#if VSG_DPP_REDUCE
+    argmin_dpp_step<0xB1>(d, id);
+    argmin_dpp_step<0x4E>(d, id);
+    argmin_dpp_step<0x141>(d, id);
+    argmin_dpp_step<0x140>(d, id);
+    float bd = readlane(d, 0);
+    uint32_t bi = readlane(id, 0);
+#pragma unroll
+    for (int r = 16; r < 64; r += 16) {
+        const float rd = readlane(d, r);
+        const uint32_t ri = readlane(id, r);
+        if (cand_less(rd, ri, bd, bi)) {
+            bd = rd;
+            bi = ri;
+        }
+    }
+    d = bd;
+    id = bi;
+#else
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         float od = __shfl_xor(d, o);
@@ -80,6 +134,7 @@ __device__ __forceinline__ void wave_argmin(float& d, uint32_t& id) {
             id = oi;
         }
     }
+#endif
 }
 
 // Query / candidate register image: lane (sub, sl) holds chunks v*G + sl.
@@ -198,8 +253,7 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
                     acc += live ? t : 0.f;
                 }
             }
-#pragma unroll
-            for (int o = G / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+            acc = group_sum0<G>(acc);
             const int r = base + u * R + sub;
             if (sl == 0 && r < count) out[r] = (MET == MET_L2) ? acc : 1.f - acc;
         }
@@ -255,11 +309,8 @@ __device__ __forceinline__ void rows_dist2(const uint8_t* __restrict__ vecs, siz
                     a1 += live ? t1 : 0.f;
                 }
             }
-#pragma unroll
-            for (int o = G / 2; o > 0; o >>= 1) {
-                a0 += __shfl_xor(a0, o);
-                a1 += __shfl_xor(a1, o);
-            }
+            a0 = group_sum0<G>(a0);
+            a1 = group_sum0<G>(a1);
             const int r = base + u * R + sub;
             if (sl == 0 && r < count) {
                 out0[r] = (MET == MET_L2) ? a0 : 1.f - a0;
@@ -326,8 +377,7 @@ __device__ __forceinline__ uint32_t rows_test(const uint8_t* __restrict__ vecs, 
             const bool ok = sl == 0 && r < count;
 #pragma unroll
             for (int j = 0; j < NQ; ++j) {
-#pragma unroll
-                for (int o = G / 2; o > 0; o >>= 1) a[j] += __shfl_xor(a[j], o);
+                a[j] = group_sum0<G>(a[j]);
                 const float d = (MET == MET_L2) ? a[j] : 1.f - a[j];
                 if (__ballot(ok && d < lim[j])) hit |= 1u << j;
             }

@@ -205,6 +205,32 @@ __device__ __forceinline__ void unpack_chunk(const uint4 raw, float (&out)[Chunk
     }
 }
 
+// One element of the metric sum, a single FMA: (x - q)^2 + acc for l2sq, x q + acc
+// for the dot products.  Chunks past the row's end (lanes of a partial shape)
+// add nothing: every register image (QReg::load / set) is zero there, so a dot
+// term is x * 0, and an l2sq term reads a row chunk zeroed first (mask_tail).
+template <int MET> __device__ __forceinline__ float metric_fma(float x, float q, float acc) {
+    if constexpr (MET == MET_L2) {
+        const float df = x - q;
+        return __builtin_fmaf(df, df, acc);
+    } else {
+        return __builtin_fmaf(x, q, acc);
+    }
+}
+// l2sq on a partial row shape (G * VM > nchunks): the clamped loads of the lanes
+// past the end repeat the last chunk, so zero them (once per row chunk, not per
+// term); a dot product needs nothing (its register image is zero there).
+template <int G, int VM, int MET>
+__device__ __forceinline__ void mask_tail(uint4 (&raw)[VM], int nchunks, int sl) {
+    if constexpr (MET == MET_L2) {
+        if (G * VM != nchunks) {
+#pragma unroll
+            for (int v = 0; v < VM; ++v)
+                if (v * G + sl >= nchunks) raw[v] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+}
+
 // Distances from the register image q to `count` rows listed in ids[] (LDS),
 // written to out[] (LDS).  Wave-uniform count.  out[r] holds the metric
 // distance (l2sq, or 1 - dot).  All U x VM chunk loads of a pass are issued
@@ -236,22 +262,13 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             float acc = 0.f;
+            mask_tail<G, VM, MET>(raw[u], nchunks, sl);
 #pragma unroll
             for (int v = 0; v < VM; ++v) {
-                const bool live = (v * G + sl) < nchunks;
                 float x[E];
                 unpack_chunk<T>(raw[u][v], x);
 #pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    float t;
-                    if constexpr (MET == MET_L2) {
-                        const float df = x[e] - q.x[v][e];
-                        t = df * df;
-                    } else {
-                        t = x[e] * q.x[v][e];
-                    }
-                    acc += live ? t : 0.f;
-                }
+                for (int e = 0; e < E; ++e) acc = metric_fma<MET>(x[e], q.x[v][e], acc);
             }
             acc = group_sum0<G>(acc);
             const int r = base + u * R + sub;
@@ -288,25 +305,15 @@ __device__ __forceinline__ void rows_dist2(const uint8_t* __restrict__ vecs, siz
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             float a0 = 0.f, a1 = 0.f;
+            mask_tail<G, VM, MET>(raw[u], nchunks, sl);
 #pragma unroll
             for (int v = 0; v < VM; ++v) {
-                const bool live = (v * G + sl) < nchunks;
                 float x[E];
                 unpack_chunk<T>(raw[u][v], x);
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
-                    float t0, t1;
-                    if constexpr (MET == MET_L2) {
-                        const float d0 = x[e] - q0.x[v][e];
-                        const float d1 = x[e] - q1.x[v][e];
-                        t0 = d0 * d0;
-                        t1 = d1 * d1;
-                    } else {
-                        t0 = x[e] * q0.x[v][e];
-                        t1 = x[e] * q1.x[v][e];
-                    }
-                    a0 += live ? t0 : 0.f;
-                    a1 += live ? t1 : 0.f;
+                    a0 = metric_fma<MET>(x[e], q0.x[v][e], a0);
+                    a1 = metric_fma<MET>(x[e], q1.x[v][e], a1);
                 }
             }
             a0 = group_sum0<G>(a0);
@@ -353,24 +360,15 @@ __device__ __forceinline__ uint32_t rows_test(const uint8_t* __restrict__ vecs, 
             float a[NQ];
 #pragma unroll
             for (int j = 0; j < NQ; ++j) a[j] = 0.f;
+            mask_tail<G, VM, MET>(raw[u], nchunks, sl);
 #pragma unroll
             for (int v = 0; v < VM; ++v) {
-                const bool live = (v * G + sl) < nchunks;
                 float x[E];
                 unpack_chunk<T>(raw[u][v], x);
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
 #pragma unroll
-                    for (int j = 0; j < NQ; ++j) {
-                        float t;
-                        if constexpr (MET == MET_L2) {
-                            const float df = x[e] - q[j].x[v][e];
-                            t = df * df;
-                        } else {
-                            t = x[e] * q[j].x[v][e];
-                        }
-                        a[j] += live ? t : 0.f;
-                    }
+                    for (int j = 0; j < NQ; ++j) a[j] = metric_fma<MET>(x[e], q[j].x[v][e], a[j]);
                 }
             }
             const int r = base + u * R + sub;
@@ -393,20 +391,12 @@ __device__ __forceinline__ float reg_dist(const QReg<G, VM, T>& a, const QReg<G,
     constexpr int E = ChunkT<T>::E;
     const int sl = lane_id() % G;
     float acc = 0.f;
+    (void)sl;
+    (void)nchunks;  // both images are zero past the row's end
 #pragma unroll
     for (int v = 0; v < VM; ++v) {
-        const bool live = (v * G + sl) < nchunks;
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            float t;
-            if constexpr (MET == MET_L2) {
-                const float df = b.x[v][e] - a.x[v][e];
-                t = df * df;
-            } else {
-                t = b.x[v][e] * a.x[v][e];
-            }
-            acc += live ? t : 0.f;
-        }
+        for (int e = 0; e < E; ++e) acc = metric_fma<MET>(b.x[v][e], a.x[v][e], acc);
     }
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);

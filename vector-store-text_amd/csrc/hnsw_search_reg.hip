@@ -34,8 +34,12 @@
 
 namespace vsg {
 
+// occupancy request (probes: -DVSG_SEARCH_ATTR='__attribute__((amdgpu_waves_per_eu(5)))')
+#ifndef VSG_SEARCH_ATTR
+#define VSG_SEARCH_ATTR
+#endif
 template <int G, int VM, int U, typename T, int MET, int R>
-__global__ __launch_bounds__(64) void hnsw_search_reg_kernel(SearchParams p) {
+__global__ __launch_bounds__(64) VSG_SEARCH_ATTR void hnsw_search_reg_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     int qi = blockIdx.x;
     if (p.xcd_map) {

@@ -4,7 +4,8 @@
 // D = X . Q^T with `v_mfma_f32_32x32x2_f32` (exact f32 FMA chain, 64 FLOP/clk/SIMD),
 // fused with a per-lane register top-KMAX so no distance tile ever reaches HBM.
 //
-//   block = 256 threads (4 waves, 2 x 2), tile = 128 base rows x 128 queries,
+//   block = 256 threads (4 waves, 2 x 2), tile = 128 base rows x 128 queries (or 4 x 1:
+//   256 rows x 64 queries for batches <= 64),
 //   K stage = 32 dims, two static LDS buffers [rows | queries][32] floats (64 KiB,
 //   XOR-swizzled 16-B slots), the next stage streamed in by LDS-DMA
 //   (global_load_lds) during the MFMAs of the current one, one barrier per stage.
@@ -29,11 +30,14 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int KT = 32;   // dims per stage = one 128-B LDS row
 constexpr int LDK = 32;  // LDS row stride (floats), unpadded: glds writes lane-linear 1-KiB pieces
-// WQ = waves along the query axis: 2 -> 128 rows x 128 queries, 256 threads;
-// 1 -> 128 rows x 64 queries, 128 threads (batches of <= 64 queries: the 128-query
-// tile computed half of its MFMAs for clamped padding queries, 0.28 of peak at 64)
-template <int WQ> struct MfmaTile {
-    static constexpr int BQ = 64 * WQ, NW = 2 * WQ, STAGE = (MFMA_BR + BQ) * LDK;
+// WQ = waves along the query axis, WR = along the row axis (64 x 64 per wave):
+//   WQ 2, WR 2 -> 128 rows x 128 queries, 256 threads (batches > 64);
+//   WQ 1, WR 4 -> 256 rows x 64 queries, 256 threads (batches <= 64: the 128-query
+//   tile computed half of its MFMAs for padding queries, 0.28 of peak at 64; the
+//   128 x 64 tile of 2 waves left one wave per SIMD and re-staged the queries
+//   for every 128 rows)
+template <int WQ, int WR> struct MfmaTile {
+    static constexpr int BQ = 64 * WQ, BR = 64 * WR, NW = WQ * WR, STAGE = (BR + BQ) * LDK;
 };
 
 // 16-B slot of logical chunk c (0..7) in LDS row R: XOR swizzle so the sixteen
@@ -60,16 +64,16 @@ __device__ __forceinline__ void topk_insert(float (&ld)[KMAX], uint32_t (&li)[KM
     }
 }
 
-template <int KMAX, int MET, int WQ>
-__global__ __launch_bounds__(128 * WQ, 2) void mfma_exact_kernel(MfmaExactParams p) {
-    using TL = MfmaTile<WQ>;
-    constexpr int BQ = TL::BQ, NW = TL::NW;
+template <int KMAX, int MET, int WQ, int WR>
+__global__ __launch_bounds__(64 * WQ * WR, 2) void mfma_exact_kernel(MfmaExactParams p) {
+    using TL = MfmaTile<WQ, WR>;
+    constexpr int BQ = TL::BQ, BR = TL::BR, NW = TL::NW;
     __shared__ __attribute__((aligned(16))) float lds_a[TL::STAGE];
     __shared__ __attribute__((aligned(16))) float lds_b[TL::STAGE];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int w = tid >> 6;
-    const int wq = WQ == 2 ? (w & 1) : 0, wr = WQ == 2 ? (w >> 1) : w;
+    const int wq = w % WQ, wr = w / WQ;
     const int h = lane >> 5, r = lane & 31;
 
     // XCD-contiguous block -> (split, query tile)
@@ -80,7 +84,7 @@ __global__ __launch_bounds__(128 * WQ, 2) void mfma_exact_kernel(MfmaExactParams
     const int split = L / p.qtiles;
     const int qt = L % p.qtiles;
     const int q0 = qt * BQ;
-    const size_t ntiles = (p.nslots + MFMA_BR - 1) / MFMA_BR;
+    const size_t ntiles = (p.nslots + BR - 1) / BR;
     const size_t t_beg = (size_t)split * p.tiles_per_split;
     const size_t t_end = min(t_beg + (size_t)p.tiles_per_split, ntiles);
     const int nst = (p.row_floats + KT - 1) / KT;
@@ -105,7 +109,7 @@ __global__ __launch_bounds__(128 * WQ, 2) void mfma_exact_kernel(MfmaExactParams
     }
 
     for (size_t tile = t_beg; tile < t_end; ++tile) {
-        const size_t r0 = tile * MFMA_BR;
+        const size_t r0 = tile * BR;
         floatx16 acc[2][2];
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -122,16 +126,16 @@ __global__ __launch_bounds__(128 * WQ, 2) void mfma_exact_kernel(MfmaExactParams
         // Addresses: a wave-uniform stage base + a 32-bit per-lane offset (row within
         // the tile, clamped, x row_floats + swizzled chunk), so no 64-bit address per
         // piece stays live across the K loop (the 64-query tile spilled with them).
-        const int xlast = (int)min((size_t)(MFMA_BR - 1), p.nslots - 1 - r0);
+        const int xlast = (int)min((size_t)(BR - 1), p.nslots - 1 - r0);
         const int qlast = min(BQ - 1, p.nq - 1 - q0);
         auto load_stage = [&](int s, float* xs) {
             const int k0 = s * KT;
-            float* qs = xs + MFMA_BR * LDK;
+            float* qs = xs + BR * LDK;
             const float* xb = p.vecs + r0 * p.row_floats + k0;
             const float* qb = p.queries + (size_t)q0 * p.row_floats + k0;
 #pragma unroll
-            for (int u = 0; u < MFMA_BR / 8 / NW; ++u) {
-                const int piece = w * (MFMA_BR / 8 / NW) + u;
+            for (int u = 0; u < BR / 8 / NW; ++u) {
+                const int piece = w * (BR / 8 / NW) + u;
                 const int R = piece * 8 + prow;
                 const uint32_t off = (uint32_t)min(R, xlast) * (uint32_t)p.row_floats + (uint32_t)swz(R, pslot) * 4;
                 __builtin_amdgcn_global_load_lds((gptr_t)(xb + off), (lptr_t)(xs + piece * 8 * LDK), 16, 0, 0);
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(128 * WQ, 2) void mfma_exact_kernel(MfmaExactParams
         auto stage = [&](int s, const float* cur, float* nxt) __attribute__((always_inline)) {
             if (s + 1 < nst) load_stage(s + 1, nxt);  // nxt was last read before the previous barrier
             const float* xs = cur;
-            const float* qs = cur + MFMA_BR * LDK;
+            const float* qs = cur + BR * LDK;
 #pragma unroll
             for (int tq = 0; tq < 4; ++tq) {
                 float4 xa[2], qb[2];
@@ -208,8 +212,8 @@ __global__ __launch_bounds__(128 * WQ, 2) void mfma_exact_kernel(MfmaExactParams
         }
     }
 
-    const int nparts = p.splits * 4;
-    const int part = (split * 2 + wr) * 2 + h;
+    const int nparts = p.splits * WR * 2;
+    const int part = (split * WR + wr) * 2 + h;
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
         const int qi = q0 + wq * 64 + b * 32 + r;
@@ -224,15 +228,16 @@ __global__ __launch_bounds__(128 * WQ, 2) void mfma_exact_kernel(MfmaExactParams
 }
 
 hipError_t launch_mfma_exact(MetricKind mk, const MfmaExactParams& p, hipStream_t s) {
-    if (p.kmax != 16 || (p.bq != 64 && p.bq != 128)) return hipErrorNotSupported;
+    // (bq, br) = (128, 128) or (64, 256); both 256-thread blocks
+    if (p.kmax != 16 || !((p.bq == 128 && p.br == 128) || (p.bq == 64 && p.br == 256))) return hipErrorNotSupported;
     const int total = p.qtiles * p.splits;
     const int nb = (total + 7) / 8 * 8;
     if (p.bq == 128) {
-        auto kern = mk == MK_L2 ? mfma_exact_kernel<16, MET_L2, 2> : mfma_exact_kernel<16, MET_DOT, 2>;
+        auto kern = mk == MK_L2 ? mfma_exact_kernel<16, MET_L2, 2, 2> : mfma_exact_kernel<16, MET_DOT, 2, 2>;
         hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, p);
     } else {
-        auto kern = mk == MK_L2 ? mfma_exact_kernel<16, MET_L2, 1> : mfma_exact_kernel<16, MET_DOT, 1>;
-        hipLaunchKernelGGL(kern, dim3(nb), dim3(128), 0, s, p);
+        auto kern = mk == MK_L2 ? mfma_exact_kernel<16, MET_L2, 1, 4> : mfma_exact_kernel<16, MET_DOT, 1, 4>;
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, p);
     }
     return hipGetLastError();
 }

@@ -699,6 +699,7 @@ static hipError_t rows_to_cells(vsg_index* h, const uint8_t* rows, const float* 
     mp.tiles_per_split = cs.tps;
     mp.kmax = 16;
     mp.bq = MFMA_BQ;
+    mp.br = MFMA_BR;
     mp.part_d = part_d;
     mp.part_i = part_i;
     hipError_t e = launch_mfma_exact(h->mk, mp, st);
@@ -1481,15 +1482,28 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
     int qtiles = 0, kmax = 0, nparts = 0, nblocks = 1, rpb = 1, ngroups = 0;
     size_t splits = 0, tps = 0, np = 0, np_lists = 0;
     const int bq = nq <= 64 ? 64 : MFMA_BQ;  // the 64-query tile for small batches
+    const int br = bq == 64 ? 256 : MFMA_BR;  // ... 256 rows deep
     if (use_mfma) {
         qtiles = (int)((nq + bq - 1) / bq);
-        const size_t ntiles = (slots + MFMA_BR - 1) / MFMA_BR;
-        splits = std::min<size_t>(ntiles, std::max<size_t>(1, (1024 + qtiles - 1) / qtiles));
+        const size_t ntiles = (slots + br - 1) / br;
+        // (query tile, row split) blocks in whole rounds of resident blocks (2 per CU:
+        // 64 / 80 KiB of LDS): 1,024 = two rounds of the 128 x 128 tile, 512 = one of
+        // the 256 x 64 tile (round 2: 1,024 blocks of a 128 x 64 tile, 1.33 rounds)
+        const size_t target = bq == 64 ? 512 : 1024;
+        splits = std::min<size_t>(ntiles, std::max<size_t>(1, (target + qtiles - 1) / qtiles));
         tps = (ntiles + splits - 1) / splits;
         splits = (ntiles + tps - 1) / tps;
         kmax = 16;
-        nparts = (int)splits * 4;
-        np = nq * (size_t)nparts * kmax;
+        // more than 64 partial lists per query: whole 64-list groups (padding splits
+        // hold no rows and write empty lists), merged in two stages
+        const size_t lists = (size_t)(br / 64) * 2;  // per split: row waves x half-waves
+        if (splits * lists > 64) {
+            splits = (splits * lists + 63) / 64 * 64 / lists;
+            ngroups = (int)(splits * lists / 64);
+        }
+        nparts = (int)(splits * lists);
+        np_lists = nq * (size_t)nparts * kmax;
+        np = np_lists + (ngroups ? nq * (size_t)ngroups * k : 0);
     } else if (exact) {
         // grid.y = row blocks (<= 65535 per dimension).  4,096-row blocks fill the
         // chip from ~32 queries on; a smaller batch gets more, shorter blocks so
@@ -1553,17 +1567,30 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         mp.tiles_per_split = (int)tps;
         mp.kmax = kmax;
         mp.bq = bq;
+        mp.br = br;
         mp.part_d = pd;
         mp.part_i = pi;
         err = launch_mfma_exact(h->mk, mp, s);
+        if (err == hipSuccess && ngroups) {  // stage 1: each 64-list group -> one k-list
+            MergeParams g1{};
+            g1.part_d = pd;
+            g1.part_i = pi;
+            g1.nq = (int)(nq * ngroups);
+            g1.parts = 64;
+            g1.k = (int)k;
+            g1.kin = kmax;
+            g1.out_part_d = pd + np_lists;
+            g1.out_part_i = pi + np_lists;
+            err = launch_merge_parts(g1, s);
+        }
         if (err == hipSuccess) {
             MergeParams gp{};
-            gp.part_d = pd;
-            gp.part_i = pi;
+            gp.part_d = ngroups ? pd + np_lists : pd;
+            gp.part_i = ngroups ? pi + np_lists : pi;
             gp.nq = (int)nq;
-            gp.parts = nparts;
+            gp.parts = ngroups ? ngroups : nparts;
             gp.k = (int)k;
-            gp.kin = kmax;
+            gp.kin = ngroups ? 0 : kmax;
             gp.keys = h->d_keys;
             gp.out_keys = ok;
             gp.out_dist = od;

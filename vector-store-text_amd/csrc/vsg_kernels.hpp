@@ -102,9 +102,10 @@ struct MfmaExactParams {
     size_t nslots;
     const uint8_t* flags;
     int qtiles, splits;
-    int tiles_per_split;    // 128-row tiles per split
+    int tiles_per_split;    // br-row tiles per split
     int kmax;
-    int bq;                 // queries per tile: 128 (256-thread blocks) or 64 (batches <= 64)
+    int bq;                 // queries per tile: 128, or 64 (batches <= 64)
+    int br;                 // base rows per tile: 128 with bq 128, 256 with bq 64
     float* part_d;
     uint32_t* part_i;
 };

@@ -858,7 +858,10 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     // first ~20 batches fill a fraction of the GPU and cost a wave's latency
     // each): a 125k-row shard (the 8-GPU layout of C2) 0.138 -> 0.122 s, C2 1M
     // 0.595 -> 0.585 s, recall unchanged (profiles/r03_build_probe.jsonl).
-    const double frac_early = env_double("VSG_BUILD_BATCH_FRAC", 2.0);
+    // Only for large calls: a small index is built entirely in this regime, where
+    // 2x batches leave each node fewer links to its own batch-mates (a 4,000-row
+    // index: recall@10 0.952 -> 0.936 at ef 64), and its build is cheap anyway.
+    const double frac_early = env_double("VSG_BUILD_BATCH_FRAC", n >= 65536 ? 2.0 : 0.5);
     const double frac = env_double("VSG_BUILD_BATCH_FRAC2", 0.5);
     const double switch_at = env_double("VSG_BUILD_BATCH_SWITCH", 8192);
     const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 65536);

@@ -17,8 +17,9 @@ if [ "$STAGE" = all ] || [ "$STAGE" = bench ]; then
   timeout -k 10 400 python3 -u bench.py > gpurun_out/r03_bench_n1.log 2>&1 || { tail -20 gpurun_out/r03_bench_n1.log; exit 1; }
   tail -c 600 gpurun_out/r03_bench_n1.log
   EF=${2:-34}
-  rm -rf gpurun_out/prof_bench
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -- python3 -u bench.py --no-cpu --upper-ef 0 --rerank-leg 0 --config-ef 0 --ef $EF --steps 10 > gpurun_out/r03_prof_bench.log 2>&1 || exit 1
-  find gpurun_out/prof_bench -name '*kernel_trace.csv' -size +20M -delete
+  P=gpurun_out/prof_bench_$(date +%s)  # one directory per run: gpurun merges outputs back
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P -- python3 -u bench.py --no-cpu --upper-ef 0 --rerank-leg 0 --config-ef 0 --ef $EF --steps 10 > gpurun_out/r03_prof_bench.log 2>&1 || exit 1
+  find $P -name '*kernel_trace.csv' -size +20M -delete
+  echo "rocprof output: $P"
 fi
 echo done

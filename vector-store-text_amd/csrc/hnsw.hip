@@ -890,7 +890,7 @@ hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipSt
     const int nw = (p.waves == 2 || p.waves == 4) && p.g.M0 <= 64 ? p.waves : 1;
     const size_t lds = search_lds_bytes(p.ef, p.hash_size, nw);
     hipError_t err = hipSuccess;
-    dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<true>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto run = [&](auto kern) {
             if (lds > 65536)
                 (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -148,7 +148,7 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
         const int r = atoi(e);
         if ((r == 2 || r == 4 || r == 8 || r == 17) && 64 * r >= p.ef + 64) rows = r;
     }
-    dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<true>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
         using T = typename decltype(tt)::T;
         constexpr int MET = decltype(mt)::MET;

@@ -63,10 +63,27 @@ inline void dispatch_shape(int nc, F&& f) {
     else f(Shape<64, 16, 1>{});
 }
 
-// f(Shape, TypeTag, MetTag)
+// The search kernels' shape: as dispatch_shape, except 5..16-chunk rows (128-d f16 --
+// C4 -- and 64-d f32) run 8 lanes x 2 chunks, 8 rows per pass: with the DPP group sums
+// one 32-row pass covers an expansion's ~20 fresh rows where 16 x 1 took two round
+// trips (C4 shard at 10k queries: -9 % at ef 64, -7 % at ef 192;
+// profiles/r03_c4_shape_probe.jsonl).  The build keeps 16 x 1 (8 x 2: +9 % build
+// time, more selection rows per pass).  Distances are the same sums in another lane
+// order: exact on integer data, within rounding otherwise.
 template <typename F>
+inline void dispatch_shape_search(int nc, F&& f) {
+    if (nc > 4 && nc <= 16) f(Shape<8, 2, 4>{});
+    else dispatch_shape(nc, f);
+}
+
+// f(Shape, TypeTag, MetTag); SEARCH selects dispatch_shape_search
+template <bool SEARCH = false, typename F>
 inline void dispatch_all(Storage st, MetricKind mk, int nc, F&& f) {
-    dispatch_shape(nc, [&](auto sh) {
+    auto pick = [&](auto&& g) {
+        if constexpr (SEARCH) dispatch_shape_search(nc, g);
+        else dispatch_shape(nc, g);
+    };
+    pick([&](auto sh) {
         if (st == ST_F32) {
             if (mk == MK_L2) f(sh, TypeTag<float>{}, MetTag<MET_L2>{});
             else f(sh, TypeTag<float>{}, MetTag<MET_DOT>{});

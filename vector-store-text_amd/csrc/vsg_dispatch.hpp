@@ -70,9 +70,12 @@ inline void dispatch_shape(int nc, F&& f) {
 // profiles/r03_c4_shape_probe.jsonl).  The build keeps 16 x 1 (8 x 2: +9 % build
 // time, more selection rows per pass).  Distances are the same sums in another lane
 // order: exact on integer data, within rounding otherwise.
+#ifndef VSG_SEARCH_SHAPE16
+#define VSG_SEARCH_SHAPE16 8, 2, 4
+#endif
 template <typename F>
 inline void dispatch_shape_search(int nc, F&& f) {
-    if (nc > 4 && nc <= 16) f(Shape<8, 2, 4>{});
+    if (nc > 4 && nc <= 16) f(Shape<VSG_SEARCH_SHAPE16>{});
     else dispatch_shape(nc, f);
 }
 

@@ -63,8 +63,9 @@ def test_c3_10m768_cos_eight_row_shards_merged():
     assert r[32] >= 0.95 and r[64] >= r[32] - 0.002
 
 
-def test_c5_1536_ip_mfma_bitexact_vs_oracle(monkeypatch):
-    n, dim, nq, k = 5000, 1536, 160, 10
+@pytest.mark.parametrize("nq", [40, 160])  # 40: the 256-row x 64-query tile, two-stage merge
+def test_c5_1536_ip_mfma_bitexact_vs_oracle(nq, monkeypatch):
+    n, dim, k = 5000, 1536, 10
     x = np.floor(G.uint8_valued(n, dim, 51) / 16.0)   # sums < 2^24: exact in f32
     q = np.floor(G.uint8_valued(nq, dim, 52) / 16.0)
     keys = np.arange(n, dtype=np.uint64) * 5 + 2
@@ -82,9 +83,10 @@ def test_c5_1536_ip_mfma_bitexact_vs_oracle(monkeypatch):
         np.testing.assert_array_equal(m.counts, oc)
 
 
-def test_c5_1m1536_ip_mfma_vs_valu_full_size(monkeypatch):
+@pytest.mark.parametrize("nq", [64, 256])  # 64: 256 x 64 tiles, ~2,900 partial lists per query
+def test_c5_1m1536_ip_mfma_vs_valu_full_size(nq, monkeypatch):
     import torch
-    n, dim, nq, k = 1_000_000, 1536, 256, 10
+    n, dim, k = 1_000_000, 1536, 10
     bs, qs, ms = G.config_seeds(4)
     x = vsg.datagen_device("clustered", n, dim, bs, ms)
     q = vsg.datagen_device("clustered", nq, dim, qs, ms)

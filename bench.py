@@ -618,15 +618,22 @@ def build_roofline(a, head):
     except (OSError, ValueError):
         pass
 
+    def tfrac(traffic, t):
+        # measured HBM bytes (PMC) over the same device time: the HBM utilisation itself
+        # (`frac` above 1 = algorithmic bytes served by L2 / MALL, not HBM)
+        return round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None
+
     def line(kernel, alg, t, traffic):
         g = alg / t / 1e9
         return {"kernel": kernel, "alg_bytes": int(alg), "kernel_s": round(t, 4), "achieved": round(g, 1),
                 "frac": round(g / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_over_alg": round(traffic / alg, 3) if traffic and alg else None}
+                "traffic_over_alg": round(traffic / alg, 3) if traffic and alg else None,
+                "traffic_frac": tfrac(traffic, t)}
 
     ach = beam_bytes / t_beam / 1e9
     return {"bound": "hbm", "kernel": "hnsw_insert_beam_kernel", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc.get("beam_hbm_bytes"),
+            "traffic_frac": tfrac(pmc.get("beam_hbm_bytes"), t_beam),
             "traffic_unit": "HBM bytes over all launches of the kernel in the build",
             "alg_bytes_insert": int(beam_bytes),
             "kernel_s": {"beam": round(t_beam, 4), "select": round(ns["select"], 4), "sort": round(ns["sort"], 4),

@@ -455,6 +455,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(head["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(head["achieved_gbs"] / HBM_PEAK_GBS, 4),
                      "traffic": pmc_traffic(a, head["ef"]) if head["mode"] != "shard" else None,
+                     "traffic_frac": (round(pmc_traffic(a, head["ef"]) / (head["kern_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                      if head["mode"] != "shard" and pmc_traffic(a, head["ef"]) else None),
                      "kernel": "hnsw_search_reg_kernel", "kernel_ms": round(head["kern_ms"], 3),
                      "alg_bytes_per_launch": int(head["alg_bytes"]),
                      "dist_evals_per_query": round(head["dist_per_query"], 1)},

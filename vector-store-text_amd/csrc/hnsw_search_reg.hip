@@ -148,7 +148,7 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
         const int r = atoi(e);
         if ((r == 2 || r == 4 || r == 8 || r == 17) && 64 * r >= p.ef + 64) rows = r;
     }
-    dispatch_all<true>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+    auto body = [&](auto sh, auto tt, auto mt) {
         constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
         using T = typename decltype(tt)::T;
         constexpr int MET = decltype(mt)::MET;
@@ -171,7 +171,11 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
         else if (rows == 4) run(hnsw_search_reg_kernel<G, VM, U, T, MET, 4>);
         else if (rows == 8) run(hnsw_search_reg_kernel<G, VM, U, T, MET, 8>);
         else run(hnsw_search_reg_kernel<G, VM, U, T, MET, 17>);
-    });
+    };
+    // the search row shape (dispatch_shape_search), except with 17 register rows
+    // (ef > 448), where the 8 x 2 shape of 64-d f32 rows spills registers
+    if (rows == 17) dispatch_all<false>(st, mk, p.g.nchunks, body);
+    else dispatch_all<true>(st, mk, p.g.nchunks, body);
     return err;
 }
 

@@ -98,6 +98,9 @@ typedef struct {
     uint64_t build_sort_ns;            /*   stream): insert (descent + beam + selection), pair sort, */
     uint64_t build_reverse_ns;         /*   reverse links -- the build roofline's time base */
     uint64_t build_select_ns;          /* the selection kernel's share of build_insert_ns (split insert) */
+    uint64_t search_filter_overflow;   /* filtered searches (index with removed entries): candidates
+                                          dropped for want of room in the candidate set; results are
+                                          usearch's exactly while this stays 0 */
 } vsg_stats_t;
 
 /* replaces usearch::Index::new(&options) — src/index/usearch.rs:98 */

@@ -409,6 +409,8 @@ typedef struct {
     uint32_t* nbr;
     cand_t* tmp;
     size_t tmp_cap;
+    cand_t* heap; /* filtered search: usearch's `next` min-heap (grows) */
+    size_t heap_cap;
     uint64_t ndist;
 } scratch_t;
 
@@ -430,6 +432,7 @@ static void scratch_free(scratch_t* s) {
     free(s->expanded);
     free(s->nbr);
     free(s->tmp);
+    free(s->heap);
 }
 
 static void free_search_scratch(orc_hnsw* h) {
@@ -533,11 +536,111 @@ static size_t beam(const orc_hnsw* h, const float* q, uint32_t ep, float dep, si
     return n;
 }
 
+static void heap_push(scratch_t* s, size_t* n, float d, uint32_t id) {
+    if (*n == s->heap_cap) {
+        s->heap_cap = s->heap_cap ? 2 * s->heap_cap : 256;
+        s->heap = (cand_t*)realloc(s->heap, s->heap_cap * sizeof(cand_t));
+    }
+    size_t i = (*n)++;
+    while (i > 0) {
+        size_t p = (i - 1) >> 1;
+        if (!cand_less(d, id, s->heap[p].d, s->heap[p].id)) break;
+        s->heap[i] = s->heap[p];
+        i = p;
+    }
+    s->heap[i].d = d;
+    s->heap[i].id = id;
+}
+
+static void heap_pop(scratch_t* s, size_t* n) {
+    cand_t last = s->heap[--(*n)];
+    size_t i = 0;
+    for (;;) {
+        size_t c = 2 * i + 1;
+        if (c >= *n) break;
+        if (c + 1 < *n && cand_less(s->heap[c + 1].d, s->heap[c + 1].id, s->heap[c].d, s->heap[c].id)) ++c;
+        if (!cand_less(s->heap[c].d, s->heap[c].id, last.d, last.id)) break;
+        s->heap[i] = s->heap[c];
+        i = c;
+    }
+    if (*n) s->heap[i] = last;
+}
+
+/* usearch search_to_find_in_base_ with index_dense's `allow` predicate
+ * (member.key != free_key_), the base-level search of an index that holds
+ * removed entries (usearch v2 series: index_dense_gt::search_ passes `allow`
+ * into index_gt::search; reference call sites src/index/usearch.rs:215, 245
+ * remove, :276 search).  Two sets, as usearch keeps them:
+ *   next -- every admitted candidate, removed or not (the min-heap that drives
+ *           the traversal: removed nodes are still expanded);
+ *   top  -- the best `ef` ADMITTED LIVE candidates (the result list).
+ * radius = the worst key of `top` (the start's key while `top` is empty);
+ * a candidate is admitted when |top| < ef or it beats the radius; the loop
+ * pops the nearest of `next` and stops when that is beyond the radius.  The
+ * start node joins `top` only when live (the predicate is checked on it too).
+ * Keys compare as (distance, slot) -- the restatement's canonical tie order.
+ * Without removed entries this is beam() (every node of `next` that is not in
+ * `top` was evicted from it and lies beyond the radius), so search_one() uses
+ * it only when the index holds tombstones.  Returns |top| (in s->list). */
+static size_t beam_filtered(const orc_hnsw* h, const float* q, uint32_t ep, float dep, size_t ef,
+                            scratch_t* s) {
+    scratch_newgen(s);
+    cand_t* L = s->list;
+    size_t n = 0, nh = 0;
+    s->stamp[ep] = s->gen;
+    heap_push(s, &nh, dep, ep);
+    float rd = dep; /* radius key */
+    uint32_t ri = ep;
+    if (!h->removed[ep]) {
+        L[0].d = dep;
+        L[0].id = ep;
+        n = 1;
+    }
+    while (nh) {
+        const cand_t c = s->heap[0];
+        if (cand_less(rd, ri, c.d, c.id)) break; /* nearest of `next` beyond the radius */
+        heap_pop(s, &nh);
+        size_t cnt = read_row(h, c.id, 0, s->nbr, 0);
+        for (size_t i = 0; i < cnt; ++i) {
+            uint32_t nb = s->nbr[i];
+            if (s->stamp[nb] == s->gen) continue;
+            s->stamp[nb] = s->gen;
+            float d = orc_distance(h->metric, q, VEC(h, nb), h->dim);
+            s->ndist++;
+            if (!(n < ef || cand_less(d, nb, rd, ri))) continue;
+            heap_push(s, &nh, d, nb);
+            if (h->removed[nb]) continue; /* traversed, never a result */
+            size_t lo = 0, hi = n;
+            while (lo < hi) {
+                size_t mid = (lo + hi) >> 1;
+                if (cand_less(L[mid].d, L[mid].id, d, nb)) lo = mid + 1;
+                else hi = mid;
+            }
+            if (n == ef) --n;
+            memmove(L + lo + 1, L + lo, (n - lo) * sizeof(cand_t));
+            L[lo].d = d;
+            L[lo].id = nb;
+            ++n;
+            rd = L[n - 1].d;
+            ri = L[n - 1].id;
+        }
+    }
+    return n;
+}
+
 /* usearch refine_ (heuristic neighbour selection): walk candidates in
  * ascending (distance, slot); keep c unless some already-kept r is closer to
- * c than the base is (dist(c, r) < dist(c, base)).  No back-fill. */
+ * c than the base is (dist(c, r) < dist(c, base)).  No back-fill.  Fewer
+ * candidates than `needed` are returned unfiltered (refine_'s early return
+ * `if (top_count < needed) return {top_data, top_count};`) -- on the forward
+ * links of a new node while the level holds fewer than M reachable nodes; a
+ * reverse-link prune always has M_l + 1 candidates. */
 static size_t select_heuristic(const orc_hnsw* h, const cand_t* C, size_t nc, size_t m,
                                uint32_t* out, scratch_t* s) {
+    if (nc < m) {
+        for (size_t i = 0; i < nc; ++i) out[i] = C[i].id;
+        return nc;
+    }
     size_t kept = 0;
     for (size_t i = 0; i < nc && kept < m; ++i) {
         int good = 1;
@@ -614,8 +717,12 @@ static void insert_slot(orc_hnsw* h, uint32_t q, scratch_t* s, int locked) {
     uint32_t* sel = (uint32_t*)malloc(h->M0 * sizeof(uint32_t));
     for (int l = (L < maxl ? L : maxl); l >= 0; --l) {
         size_t n = beam(h, vq, ep, dep, h->efC, l, s, locked);
+        /* usearch connect_new_node_: refine_(metric, config_.connectivity, ...)
+         * on EVERY level -- a new node keeps at most M outgoing links, level 0
+         * included; its level-0 row (M0 = 2M slots) fills up to M0 only through
+         * other nodes' reverse links (reconnect_neighbor_nodes_, add_reverse). */
+        size_t k = select_heuristic(h, s->list, n, h->M, sel, s);
         size_t m = ROWLEN(h, l);
-        size_t k = select_heuristic(h, s->list, n, m, sel, s);
         if (locked) pthread_mutex_lock(&h->node_locks[q]);
         uint32_t* r = ROW(h, q, l);
         for (size_t i = 0; i < m; ++i) r[i] = i < k ? sel[i] : ORC_EMPTY;
@@ -757,10 +864,10 @@ static void search_one(void* p, size_t qi, int tid) {
         float dep = orc_distance(h->metric, q, VEC(h, ep), h->dim);
         s->ndist++;
         for (int l = h->max_level; l >= 1; --l) ep = greedy(h, q, ep, &dep, l, s, 0);
-        size_t n = beam(h, q, ep, dep, c->ef, 0, s, 0);
+        /* removed entries: traversed, never admitted into the result list */
+        size_t n = h->live < h->slots ? beam_filtered(h, q, ep, dep, c->ef, s) : beam(h, q, ep, dep, c->ef, 0, s, 0);
         for (size_t i = 0; i < n && cnt < c->k; ++i) {
             uint32_t id = s->list[i].id;
-            if (h->removed[id]) continue;
             ok[cnt] = h->keys[id];
             od[cnt] = s->list[i].d;
             ++cnt;

@@ -71,6 +71,7 @@ pub struct vsg_stats_t {
     pub build_sort_ns: u64,
     pub build_reverse_ns: u64,
     pub build_select_ns: u64,
+    pub search_filter_overflow: u64,
 }
 
 /// The native actor's options (src/index/usearch.rs:60-66, 101-118 constants made knobs).

@@ -41,7 +41,7 @@ def test_version_and_error_strings():
 def test_options_struct_layout_matches_header():
     # vsg_index_options_t: 8 x u32/i32 + u64 = 40 bytes
     assert C.sizeof(_lib.Options) == 40
-    assert C.sizeof(_lib.Stats) == 16 * 8  # vsg_stats_t: 16 x u64 (build_select_ns since round 3)
+    assert C.sizeof(_lib.Stats) == 17 * 8  # vsg_stats_t: 17 x u64 (search_filter_overflow since round 4)
 
 
 def test_invalid_options_rejected_without_device():

@@ -179,3 +179,94 @@ def test_level_sampling_distribution():
     # P(level >= 1) = 1/M for the 1/ln(M) multiplier
     assert abs((lv >= 1).mean() - 1 / 16) < 0.01
     assert lv.max() <= 30
+
+
+# ------------------------------------------- usearch v2 semantics (round 4) --
+
+def test_oracle_new_node_keeps_at_most_M_forward_links():
+    """usearch connect_new_node_ refines with config_.connectivity (M) on every
+    level: a node's own level-0 row holds <= M entries until other nodes' reverse
+    links land (reconnect_neighbor_nodes_ fills it up to M0 = 2M)."""
+    M, n = 8, 1200
+    x = G.uint8_valued(n + 10, 24, 101).astype(np.float32)
+    h = O.HnswOracle(24, "l2sq", M, 64, 32, seed=13)
+    h.add(np.arange(n), x[:n], threads=1)
+    for i in range(10):  # the newest node has only its forward links
+        h.add([n + i], x[n + i:n + i + 1], threads=1)
+        g = h.export()
+        row = g["adj0"][n + i]
+        assert (row != 0xFFFFFFFF).sum() <= M
+        for l in range(1, int(g["levels"][n + i]) + 1):
+            up = g["upper"][int(g["upper_off"][n + i]) + l - 1]
+            assert (up != 0xFFFFFFFF).sum() <= M
+    fill = (g["adj0"] != 0xFFFFFFFF).sum(1)
+    assert fill.max() <= 2 * M and fill.max() > M  # reverse links still fill to M0
+
+
+def test_oracle_refine_early_return_complete_small_graph():
+    """refine_ returns fewer than `needed` candidates unfiltered: while the graph
+    holds fewer than M nodes every new node links to all of them, and the reverse
+    links (rows below M0) append, so M nodes form a complete graph (the heuristic
+    would drop some: clustered data has close pairs)."""
+    M = 16
+    x = G.clustered(M, 32, 5, 6)
+    h = O.HnswOracle(32, "l2sq", M, 64, 32, seed=2)
+    h.add(np.arange(M), x, threads=1)
+    g = h.export()
+    for i in range(M):
+        row = g["adj0"][i]
+        assert sorted(row[row != 0xFFFFFFFF].tolist()) == [j for j in range(M) if j != i]
+
+
+@pytest.mark.parametrize("frac", [0.3, 0.7])
+def test_oracle_removed_entries_are_traversed_not_returned(frac):
+    """index_dense's `allow` predicate: removed nodes never take a result slot,
+    so k live results come back at ef = k even with 70 % tombstones (a
+    post-filter of the ef-beam would return about (1 - frac) k)."""
+    n, dim = 4000, 32
+    x = G.uint8_valued(n, dim, 111).astype(np.float32)
+    q = G.uint8_valued(100, dim, 112).astype(np.float32)
+    h = O.HnswOracle(dim, "l2sq", 16, 64, 10, seed=1)
+    h.add(np.arange(n), x)
+    rm = np.random.default_rng(3).choice(n, int(frac * n), replace=False)
+    h.remove(rm)
+    k, d, c = h.search(q, 10, 10)
+    assert (c == 10).all()
+    assert not np.isin(k.astype(np.int64), rm).any()
+    assert (np.diff(d, axis=1) >= 0).all()
+
+
+@pytest.mark.parametrize("frac", [0.0, 0.4, 0.8])
+def test_oracle_matches_literal_usearch_loops(frac):
+    """The C restatement (set formulation, (distance, slot) keys) against a
+    literal transcription of usearch's heap loops (tests/usearch_literal.py:
+    search_to_insert_, refine_, reconnect_neighbor_nodes_, search_for_one_,
+    search_to_find_in_base_ with the `allow` predicate) on float data (no
+    ties): identical graph, identical results with tombstones."""
+    import usearch_literal as UL
+    n, dim, M, efc = 400, 12, 6, 24
+    x = G.clustered(n, dim, 7, 8)
+    q = G.clustered(40, dim, 9, 8)
+    h = O.HnswOracle(dim, "l2sq", M, efc, 16, seed=17)
+    h.add(np.arange(n), x, threads=1)
+    lit = UL.LiteralHnsw(dim, "l2sq", M, efc, seed=17)
+    for i in range(n):
+        lit.add(i, x[i])
+    g = h.export()
+    assert (g["entry"], g["max_level"]) == (lit.entry, lit.max_level)
+    for s in range(n):
+        for l in range(int(g["levels"][s]) + 1):
+            if l == 0:
+                row = g["adj0"][s]
+            else:
+                row = g["upper"][int(g["upper_off"][s]) + l - 1]
+            assert row[row != 0xFFFFFFFF].tolist() == lit.links[s][l], (s, l)
+    rm = np.random.default_rng(5).choice(n, int(frac * n), replace=False)
+    h.remove(rm)
+    lit.remove(rm)
+    for ef in (6, 16, 50):
+        k, d, c = h.search(q, 6, ef)
+        for i in range(len(q)):
+            lk, ld = lit.search(q[i], 6, ef)
+            assert k[i][: int(c[i])].tolist() == lk, (ef, i)
+            np.testing.assert_array_equal(d[i][: int(c[i])], np.array(ld, np.float32))

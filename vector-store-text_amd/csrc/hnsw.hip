@@ -106,6 +106,7 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
 
 // usearch refine_ restated (oracle select_heuristic()): walk the sorted list,
 // keep c unless a kept r has dist(c, r) < dist(c, base).  Returns #kept.
+// Fewer than m candidates: all of them, unfiltered (refine_'s early return).
 // Candidates go in blocks of NQ held in VGPRs: the block is tested against the
 // kept set in one pass over its rows (each row loaded once, rows_test), then
 // each candidate, in list order, against the block's earlier kept candidates
@@ -171,6 +172,16 @@ __device__ int select_heuristic(const GraphDev& g, WaveLds& w, int n, int m, uin
     constexpr int BLK = (64 / G) * UT;
     const int lane = lane_id();
     List& L = w.list;
+    if (n < m) {
+        // refine_'s early return (top_count < needed): every candidate, unfiltered
+        // (a new node's forward links while the level has < M reachable nodes)
+        for (int j = lane; j < n; j += 64) {
+            w.sel[j] = L.I()[j] & VSG_ID_MASK;
+            w.seld[j] = L.D()[j];
+        }
+        wave_sync();
+        return n;
+    }
     int kept = 0;
     using Q = QReg<G, VM, T>;
     for (int i = 0; i < n && kept < m; i += NQ) {
@@ -495,9 +506,12 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
         } else {
             beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, pf);
         }
+        // usearch connect_new_node_: at most M forward links on every level
+        // (refine_ with config_.connectivity); level-0 rows reach M0 = 2M only
+        // through reverse links (hnsw_reverse_kernel)
         const int m = l == 0 ? g.M0 : g.M;
         const uint64_t ts = VSG_CLK();
-        const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, m, nsel_d);
+        const int nsel = select_heuristic<G, VM, U, T, MET>(g, w, w.list.size, g.M, nsel_d);
         tsel += VSG_CLK() - ts;
         write_row(g, node, l, m, nsel, w);
         for (int j = lane; j < nsel; j += 64) {
@@ -611,8 +625,8 @@ __global__ __launch_bounds__(64) VSG_SEL_WAVES void hnsw_insert_select_kernel(In
         w.list.cur = 0;
         w.list.size = n;
         wave_sync();
-        const int m = l == 0 ? g.M0 : g.M;
-        const int nsel = select_heuristic<G, VM, U, T, MET, VSG_SEL_U_INSERT>(g, w, n, m, nsel_d);
+        const int m = l == 0 ? g.M0 : g.M;  // row width; <= M forward links (connect_new_node_)
+        const int nsel = select_heuristic<G, VM, U, T, MET, VSG_SEL_U_INSERT>(g, w, n, g.M, nsel_d);
         write_row(g, node, l, m, nsel, w);
         for (int j = lane; j < nsel; j += 64) {
             const uint64_t key = ((uint64_t)l << PAIR_L_SHIFT) | ((uint64_t)w.sel[j] << PAIR_V_SHIFT) |
@@ -866,7 +880,10 @@ __global__ __launch_bounds__(64) void edge_dist_fill_kernel(DevGraph gd, const i
 hipError_t launch_edge_dist_fill(Storage st, MetricKind mk, const DevGraph& g, const int8_t* levels, size_t n,
                                  hipStream_t s) {
     if (n == 0) return hipSuccess;
-    if (!g.adjd0 || !g.upperd) return hipErrorInvalidValue;
+    // upperd is read only for slots with levels > 0, which exist only when the
+    // graph has upper rows (and then ensure_upper allocated it): a graph without
+    // upper rows (a small loaded / imported index) has none to fill
+    if (!g.adjd0) return hipErrorInvalidValue;
     hipError_t err = hipSuccess;
     dispatch_all(st, mk, g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(edge_dist_fill_kernel, sh, tt, mt);
@@ -882,6 +899,8 @@ bool shape_supported(int nchunks) { return nchunks >= 1 && nchunks <= 1024; }
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s) {
     if (p.nq <= 0) return hipSuccess;
+    // an index with removed entries: usearch's filtered base-level search
+    if (p.filt) return launch_search_filt(st, mk, p, s);
     // register kernel up to ef 1024 (multi-entry descent: register kernel only);
     // above it the sorted LDS list (ef <= MAX_EF)
     if ((p.reg && p.ef <= (int)MAX_REG_EF) || p.upper_ef > 1) return launch_search_reg(st, mk, p, s);

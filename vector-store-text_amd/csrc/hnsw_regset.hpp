@@ -119,7 +119,10 @@ template <int R> struct RegSet {
     // iff at least `need` keys share its higher bits and have 0 there.  The
     // slot word is only selected on when several kept candidates tie on the
     // cut distance (then `need` < their count).
-    __device__ __forceinline__ void compact(int keep) {
+    // excl (filtered search): slots whose keys are not counted -- removed nodes;
+    // the cut is then the keep-th smallest counted key, every key above it (of
+    // either kind) is dropped, and the size is recounted.
+    __device__ __forceinline__ void compact(int keep, uint32_t excl = 0) {
         uint32_t ph = 0;
         int need = keep;
 #if VSG_COMPACT_EARLY
@@ -138,7 +141,7 @@ template <int R> struct RegSet {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t hi = (uint32_t)(k[r] >> 32);
-                c += popc64(__ballot(k[r] != VSG_KEY_EMPTY && (hi & hm) == ph && !((hi >> b) & 1u)));
+                c += popc64(__ballot(k[r] != VSG_KEY_EMPTY && !((excl >> r) & 1u) && (hi & hm) == ph && !((hi >> b) & 1u)));
             }
             if (c < need) {
                 need -= c;
@@ -168,14 +171,15 @@ template <int R> struct RegSet {
         }
         int ceq = 0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) ceq += popc64(__ballot(k[r] != VSG_KEY_EMPTY && (uint32_t)(k[r] >> 32) == ph));
+        for (int r = 0; r < R; ++r)
+            ceq += popc64(__ballot(k[r] != VSG_KEY_EMPTY && !((excl >> r) & 1u) && (uint32_t)(k[r] >> 32) == ph));
         uint64_t cut;
         if (need == ceq) {
             // every key on the cut distance stays: the cut is the largest of them
             uint64_t mx = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                if (k[r] != VSG_KEY_EMPTY && (uint32_t)(k[r] >> 32) == ph && k[r] > mx) mx = k[r];
+                if (k[r] != VSG_KEY_EMPTY && !((excl >> r) & 1u) && (uint32_t)(k[r] >> 32) == ph && k[r] > mx) mx = k[r];
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
                 const uint64_t w = shfl_xor64(mx, o);
@@ -191,8 +195,8 @@ template <int R> struct RegSet {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t lo = (uint32_t)k[r];
-                    c += popc64(__ballot(k[r] != VSG_KEY_EMPTY && (uint32_t)(k[r] >> 32) == ph && (lo & hm) == pl &&
-                                         !((lo >> b) & 1u)));
+                    c += popc64(__ballot(k[r] != VSG_KEY_EMPTY && !((excl >> r) & 1u) && (uint32_t)(k[r] >> 32) == ph &&
+                                         (lo & hm) == pl && !((lo >> b) & 1u)));
                 }
                 if (c < need) {
                     need -= c;
@@ -207,7 +211,14 @@ template <int R> struct RegSet {
                 k[r] = VSG_KEY_EMPTY;
                 expm &= ~(1u << r);
             }
-        size = keep;
+        if (excl) {
+            int c = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) c += popc64(__ballot(k[r] != VSG_KEY_EMPTY));
+            size = c;
+        } else {
+            size = keep;
+        }
         tkey = cut;
     }
 
@@ -349,6 +360,252 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
     }
 }
 
+
+// ------------------------------------------------ filtered base-level search --
+// usearch's base-level search of an index holding removed entries
+// (search_to_find_in_base_ with index_dense's `allow` predicate, restated in
+// oracle beam_filtered()): every admitted candidate joins `next` and is
+// expanded in key order, removed or not; only live ones join `top`, the best ef
+// admitted live keys; radius = worst key of `top` (the start's key while `top`
+// is empty); a candidate is admitted when |top| < ef or below the radius; the
+// traversal stops when the nearest unexpanded candidate is beyond the radius.
+//
+// In the register set: B holds live and removed keys (remm marks the removed
+// slots).  live_below(a) >= ef <=> a lies beyond the ef-th smallest live key,
+// the radius of a full `top` (B's ef smallest live keys are exactly `top`: an
+// over-admitted live key exceeds the radius of its admission, and the radius
+// only falls once `top` is full); while fewer than ef live keys are in B no live
+// key has left it, so the radius is the largest one (maxlive).  Unexpanded keys
+// of B at or below the radius are exactly usearch's unexpanded `next` entries at
+// or below it -- an over-admitted removed key lies beyond the radius forever --
+// so both expand the same node or both stop.  Compaction keeps the ef smallest
+// live keys and every key below the ef-th; expanded removed keys carry no
+// state (a forgotten id evaluated again only repeats an expansion whose
+// candidates are all known) and are dropped first.
+struct FiltState {
+    uint32_t remm;     // bit r: slot r of this lane holds a removed node
+    int nlive;         // live keys in B (wave-uniform)
+    uint64_t maxlive;  // largest live key in B while nlive < ef
+    uint64_t rad0;     // the start's key: the radius while no live key is admitted
+    uint32_t overflow; // candidates / keys dropped for want of room (0 in the tests)
+};
+
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) { return ~wave_min64(~v); }
+
+// #live keys of B below x (wave-uniform)
+template <int R> __device__ __forceinline__ int live_below(const RegSet<R>& B, const FiltState& F, uint64_t x) {
+    int c = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) c += popc64(__ballot(B.k[r] < x && !((F.remm >> r) & 1u)));
+    return c;
+}
+
+template <int R> __device__ __forceinline__ void recount(RegSet<R>& B, FiltState& F) {
+    int c = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const bool e = B.k[r] == VSG_KEY_EMPTY;
+        if (e) {
+            F.remm &= ~(1u << r);
+            B.expm &= ~(1u << r);
+        }
+        c += popc64(__ballot(!e));
+    }
+    B.size = c;
+}
+
+// Make room in B: expanded removed keys go; with >= ef live keys, every key
+// beyond the ef-th live key goes (tkey = that key, the radius).
+template <int R> __device__ __forceinline__ void compact_filt(RegSet<R>& B, FiltState& F, int ef) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if ((F.remm & B.expm) >> r & 1u) B.k[r] = VSG_KEY_EMPTY;
+    recount(B, F);
+    if (F.nlive >= ef) {
+        B.compact(ef, F.remm);  // drops keys above the cut; recounts the size
+        F.nlive = ef;
+        recount(B, F);
+    }
+}
+
+// place the nc staged keys sk[0..nc) (removed flags sf[]) into free slots
+template <int R>
+__device__ __forceinline__ void fill_filt(RegSet<R>& B, FiltState& F, const uint64_t* sk, const uint32_t* sf, int nc) {
+    int acc = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (acc < nc) {
+            const bool fr = B.k[r] == VSG_KEY_EMPTY;
+            const uint64_t em = __ballot(fr);
+            const int idx = acc + lanes_below(em);
+            if (fr && idx < nc) {
+                B.k[r] = sk[idx];
+                B.expm &= ~(1u << r);
+                if (sf[idx]) F.remm |= 1u << r;
+                else F.remm &= ~(1u << r);
+            }
+            acc += popc64(em);
+        }
+    }
+    B.size += nc;
+}
+
+// Admit this lane's candidate (key ck, removed flag rem) if `mine`.
+template <int R>
+__device__ __forceinline__ void admit_filt(RegSet<R>& B, FiltState& F, bool mine, uint64_t ck, bool rem, bool lossy,
+                                           int ef, uint64_t* sk, uint32_t* sf) {
+    const int lane = lane_id();
+    // |top| < ef admits everything (tkey is open until a compaction with >= ef
+    // live keys sets it to the radius; it only over-admits)
+    bool valid = mine && ck < B.tkey;
+    uint64_t vm = __ballot(valid);
+    if (lossy && vm) {
+        for (uint64_t mm = vm; mm; mm &= mm - 1) {
+            const int j = __builtin_ctzll(mm);
+            if (B.contains(readlane64(ck, j))) vm &= ~(1ull << j);
+        }
+        valid = (vm >> lane) & 1ull;
+    }
+    int nc = popc64(vm);
+    if (nc && B.size + nc > 64 * R) {
+        compact_filt(B, F, ef);
+        valid = valid && ck < B.tkey;
+        vm = __ballot(valid);
+        nc = popc64(vm);
+        if (B.size + nc > 64 * R) {
+            // No room even so: more removed nodes pending than the set holds.
+            // Drop (and count) the removed keys of B, then removed candidates --
+            // the register class is sized from the index's removed fraction so
+            // that this does not happen (stats[13]; 0 in every test).
+            const uint64_t before = (uint64_t)B.size;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if ((F.remm >> r) & 1u) B.k[r] = VSG_KEY_EMPTY;
+            recount(B, F);
+            F.overflow += (uint32_t)(before - (uint64_t)B.size);
+            if (B.size + nc > 64 * R) {
+                const bool drop = valid && rem;
+                F.overflow += (uint32_t)popc64(__ballot(drop));
+                valid = valid && !rem;
+                vm = __ballot(valid);
+                nc = popc64(vm);
+            }
+        }
+    }
+    if (nc) {
+        if (valid) {
+            sk[lanes_below(vm)] = ck;
+            sf[lanes_below(vm)] = rem ? 1u : 0u;
+        }
+        wave_sync();
+        fill_filt(B, F, sk, sf, nc);
+        wave_sync();
+        const bool lv = valid && !rem;
+        const int nl = popc64(__ballot(lv));
+        if (nl && F.nlive < ef) F.maxlive = max(F.maxlive, wave_max64(lv ? ck : 0ull));
+        F.nlive += nl;
+    }
+}
+
+// Filtered beam on level 0 (oracle beam_filtered()).  flags: slot -> bit 0 =
+// removed.  ep == VSG_EMPTY: B already holds a seed set (opt-in multi-entry
+// descent); its removed flags are read here and the radius while no seed is
+// live is the largest seed key.
+template <int G, int VM, int U, typename T, int MET, int R>
+__device__ __forceinline__ void beam_reg_filt(const GraphDev& g, const QReg<G, VM, T>& q, const uint8_t* flags,
+                                              uint32_t ep, float dep, int ef, WaveLds& w, RegSet<R>& B, FiltState& F,
+                                              uint64_t& ndist, uint64_t& nadj, BeamProf& pf) {
+    const int lane = lane_id();
+    const int m0r = __builtin_amdgcn_readfirstlane(g.M0);
+    const uint32_t* adj0 = g.adj0;
+    w.vis.clear();
+    F.remm = 0;
+    F.overflow = 0;
+    if (ep != VSG_EMPTY) {
+        if (lane == 0) {
+            bool unrec;
+            w.vis.insert(ep, unrec);
+        }
+        const uint64_t k0 = cand_key(dep, ep);
+        B.init(k0);
+        const bool r0 = flags[ep] & 1;
+        if (r0 && lane == 0) F.remm = 1u;
+        F.nlive = r0 ? 0 : 1;
+        F.maxlive = r0 ? 0ull : k0;
+        F.rad0 = k0;
+    } else {
+        wave_sync();
+        uint64_t mx = 0, ml = 0;
+        int nl = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool has = B.k[r] != VSG_KEY_EMPTY;
+            bool rm = false;
+            if (has) {
+                const uint32_t s = (uint32_t)B.k[r] & VSG_ID_MASK;
+                bool unrec;
+                w.vis.insert(s, unrec);
+                rm = flags[s] & 1;
+                mx = B.k[r] > mx ? B.k[r] : mx;
+                if (!rm) ml = B.k[r] > ml ? B.k[r] : ml;
+            }
+            if (rm) F.remm |= 1u << r;
+            nl += popc64(__ballot(has && !rm));
+        }
+        B.expm = 0;
+        B.tkey = VSG_KEY_EMPTY;
+        F.nlive = nl;
+        F.maxlive = wave_max64(ml);
+        F.rad0 = wave_max64(mx);
+    }
+    bool lossy = false;
+    uint64_t* sk = reinterpret_cast<uint64_t*>(w.sd);  // sd + si: 64 x 8 B
+    uint32_t* sf = reinterpret_cast<uint32_t*>(w.tdist);
+    wave_sync();
+    for (;;) {
+        const uint64_t t0 = VSG_CLK();
+        const uint64_t a = B.min_unexpanded();
+        if (a == VSG_KEY_EMPTY) break;
+        if (F.nlive >= ef) {
+            if (live_below(B, F, a) >= ef) break;  // beyond the ef-th live key
+        } else if (a > (F.nlive ? F.maxlive : F.rad0)) {
+            break;
+        }
+        B.mark_expanded(a);
+        const uint32_t na = (uint32_t)a & VSG_ID_MASK;
+        const uint32_t* row = adj0 + (size_t)na * m0r;
+        ++nadj;
+        for (int c0 = 0; c0 < m0r; c0 += 64) {
+            const uint32_t nb = c0 + lane < m0r ? row[c0 + lane] : VSG_EMPTY;
+            const bool full = __ballot(nb != VSG_EMPTY) == ~0ull;
+            bool fresh = false, evicted = false;
+            if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
+            const uint64_t mask = __ballot(fresh);
+            lossy = lossy || __ballot(evicted) != 0;
+            const int cnt = popc64(mask);
+            if (fresh) w.todo[lanes_below(mask)] = nb;
+            wave_sync();
+            const uint64_t t1 = VSG_CLK();
+            pf.adj += t1 - t0;
+            if (cnt) {
+                // the removed flag of this lane's candidate, loaded under the rows
+                const uint32_t cid = lane < cnt ? w.todo[lane] : 0u;
+                const uint8_t cfl = lane < cnt ? flags[cid] : (uint8_t)0;
+                rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
+                wave_sync();
+                ndist += (uint64_t)cnt;
+                const uint64_t ck = lane < cnt ? cand_key(w.tdist[lane], cid) : VSG_KEY_EMPTY;
+                const bool crm = lane < cnt && (cfl & 1);
+                wave_sync();
+                const uint64_t t2 = VSG_CLK();
+                pf.dist += t2 - t1;
+                admit_filt<R>(B, F, lane < cnt, ck, crm, lossy, ef, sk, sf);
+                pf.merge += VSG_CLK() - t2;
+            }
+            if (!full) break;
+        }
+    }
+}
 
 // The top min(ef, |B|) keys of B in ascending order into w.list (buffer 0),
 // as the LDS-list beam leaves them (the heuristic selection walks it).  B is

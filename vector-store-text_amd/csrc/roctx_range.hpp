@@ -1,8 +1,10 @@
 // roctx_range.hpp — a roctx range around every C-ABI entry point (SURVEY §5:
 // "roctx ranges around each C-ABI call"), so `rocprofv3 --marker-trace` shows
-// which library call a kernel belongs to.  Without a profiler attached the
-// push / pop are a few nanoseconds each.
+// which library call a kernel belongs to.  Built in only with -DVSG_ROCTX
+// (`make ROCTX=1`): production builds and the Rust / Python consumers do not
+// depend on the profiler SDK; without the flag VSG_RANGE() is empty.
 #pragma once
+#ifdef VSG_ROCTX
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 namespace vsg {
@@ -15,3 +17,6 @@ struct RoctxRange {
 }  // namespace vsg
 
 #define VSG_RANGE() ::vsg::RoctxRange vsg_range__(__func__)
+#else
+#define VSG_RANGE() ((void)0)
+#endif

@@ -14,7 +14,9 @@
 
 #define VSG_EMPTY 0xFFFFFFFFu
 #define VSG_EXP_BIT 0x80000000u
-#define VSG_ID_MASK 0x7FFFFFFFu
+// list entry of a removed node (filtered search: traversed, never a result)
+#define VSG_REM_BIT 0x40000000u
+#define VSG_ID_MASK 0x3FFFFFFFu  // slots < MAX_SLOTS = 2^29
 
 namespace vsg {
 
@@ -512,7 +514,9 @@ struct List {
     // distinct ids that are not in the list unless `maybe_dup` is set for them.
     // sd/si: 64-entry LDS scratch.  Returns the lowest position a candidate
     // took (entries below it are unchanged), or INT_MAX if none was placed.
-    __device__ int merge(bool valid, float cd, uint32_t ci, bool maybe_dup, float* sd, uint32_t* si) {
+    // cflag: bits stored with this lane's entry (VSG_REM_BIT; never compared).
+    __device__ int merge(bool valid, float cd, uint32_t ci, bool maybe_dup, float* sd, uint32_t* si,
+                         uint32_t cflag = 0) {
         const int lane = lane_id();
         if (valid && size == cap) {
             const float wd = D()[size - 1];
@@ -563,7 +567,7 @@ struct List {
         }
         if (valid && pos_new < cap) {
             nd[pos_new] = cd;
-            ni[pos_new] = ci;
+            ni[pos_new] = ci | cflag;
         }
         size = min(size + nc, cap);
         cur ^= 1;

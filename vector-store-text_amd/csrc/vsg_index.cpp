@@ -802,12 +802,17 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     if (edge_dist && !h->adjd_valid) {
         // the graph came from import / load: fill the distances of rows [0, s0)
         if (s0) {
+            if (h->upper_used > 0 && !h->d_upperd)
+                return fail(VSG_EDEVICE, "edge distances: upper rows without a distance table");
             int8_t* dl = nullptr;
             HIP_TRY(dev_alloc(&dl, s0));
-            HIP_TRY(hipMemcpyAsync(dl, h->h_levels.data(), s0, hipMemcpyHostToDevice, st));
-            HIP_TRY(launch_edge_dist_fill(h->st, h->mk, h->graph(true), dl, s0, st));
-            HIP_TRY(hipStreamSynchronize(st));
+            // dl freed on every path (the launch and sync may fail)
+            hipError_t e = hipMemcpyAsync(dl, h->h_levels.data(), s0, hipMemcpyHostToDevice, st);
+            if (e == hipSuccess) e = launch_edge_dist_fill(h->st, h->mk, h->graph(true), dl, s0, st);
+            const hipError_t es = hipStreamSynchronize(st);
+            if (e == hipSuccess) e = es;
             hipFree(dl);
+            if (e != hipSuccess) return fail(VSG_EDEVICE, std::string("edge distances: ") + hipGetErrorString(e));
         }
         h->adjd_valid = true;
     }
@@ -900,11 +905,12 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
                     break;
                 }
             }
-            // pair offsets: each node emits <= M0 + min(L, maxl) * M pairs
+            // pair offsets: each node emits <= M pairs per level it links on
+            // (usearch connect_new_node_ keeps <= M forward links, level 0 included)
             uint32_t acc = 0, lacc = 0;
             for (size_t j = 0; j < b; ++j) {
                 pair_off[i + j] = acc;
-                acc += (uint32_t)(h->M0 + std::min<int>(blev[i + j], maxl) * h->M);
+                acc += (uint32_t)((std::min<int>(blev[i + j], maxl) + 1) * h->M);
                 if (split) {
                     list_off[i + j] = lacc;
                     lacc += (uint32_t)(std::min<int>(blev[i + j], maxl) + 1);
@@ -1199,8 +1205,8 @@ int vsg_index_new(const vsg_index_options_t* o, vsg_index_t** out) {
         delete h;
         return fail(VSG_EDEVICE, "hipStreamCreate failed");
     }
-    if (hipMalloc(&h->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&h->d_stats, VSG_NSTATS * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(h->d_stats, 0, VSG_NSTATS * sizeof(unsigned long long)) != hipSuccess) {
         delete h;
         return fail(VSG_ENOMEM, "stats allocation failed");
     }
@@ -1635,6 +1641,12 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         // VSG_SEARCH_REG=0 selects the LDS-list kernels
         p.reg = env_double("VSG_SEARCH_REG", 1) != 0 ? 1 : 0;
         p.upper_ef = upper_ef;
+        // removed entries among the published slots (tombstones, rolled-back
+        // adds): usearch's `allow` predicate -- traversed, never results
+        if (slots > h->live) {
+            p.filt = 1;
+            p.removed_frac = (float)((double)(slots - h->live) / (double)slots);
+        }
         if (!rerank) {
             err = launch_search(h->st, h->mk, p, s);
         } else {
@@ -1852,6 +1864,23 @@ int vsg_index_exact_search(vsg_index_t* h, const float* queries, size_t nq, size
     return search_host(h, queries, nq, k, 0, out_keys, out_distances, out_counts, true);
 }
 
+// A search enqueued on a caller's stream is always either fenced or finished
+// when the call returns: if the completion event cannot be recorded, or the call
+// failed after enqueuing part of its work, wait for the stream instead -- a
+// later reserve / compaction must never free memory such a search still reads.
+static int fence_search(vsg_index* h, int rc, size_t nq, hipStream_t s) {
+    if (!nq) return rc;
+    if (rc == VSG_OK && h->fence.record(s) == hipSuccess) return VSG_OK;
+    const std::string msg = g_last_error;
+    const hipError_t e = hipStreamSynchronize(s);
+    if (rc != VSG_OK) {
+        g_last_error = msg;
+        return rc;
+    }
+    if (e != hipSuccess) return fail(VSG_EDEVICE, std::string("search: ") + hipGetErrorString(e));
+    return VSG_OK;
+}
+
 int vsg_index_search_device(vsg_index_t* h, const float* q, size_t nq, size_t k, size_t ef, uint64_t* ok,
                             float* od, uint32_t* oc, void* stream) {
     VSG_RANGE();
@@ -1859,8 +1888,7 @@ int vsg_index_search_device(vsg_index_t* h, const float* q, size_t nq, size_t k,
     std::shared_lock<std::shared_mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     const int rc = search_device_locked(h, q, nq, k, ef, ok, od, oc, (hipStream_t)stream, false);
-    if (rc == VSG_OK && nq) HIP_TRY(h->fence.record((hipStream_t)stream));
-    return rc;
+    return fence_search(h, rc, nq, (hipStream_t)stream);
 }
 
 int vsg_index_exact_search_device(vsg_index_t* h, const float* q, size_t nq, size_t k, uint64_t* ok, float* od,
@@ -1870,8 +1898,7 @@ int vsg_index_exact_search_device(vsg_index_t* h, const float* q, size_t nq, siz
     std::shared_lock<std::shared_mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     const int rc = search_device_locked(h, q, nq, k, 0, ok, od, oc, (hipStream_t)stream, true);
-    if (rc == VSG_OK && nq) HIP_TRY(h->fence.record((hipStream_t)stream));
-    return rc;
+    return fence_search(h, rc, nq, (hipStream_t)stream);
 }
 
 int vsg_merge_topk_device(const uint64_t* keys, const float* dist, size_t parts, size_t nq, size_t k_in,
@@ -1887,7 +1914,7 @@ int vsg_merge_topk_device(const uint64_t* keys, const float* dist, size_t parts,
 int vsg_index_stats(const vsg_index_t* h, vsg_stats_t* out) {
     if (!h || !out) return fail(VSG_EINVAL, "null argument");
     DeviceGuard dg(h->device);
-    unsigned long long s[16];
+    unsigned long long s[VSG_NSTATS];
     HIP_TRY(hipMemcpy(s, h->d_stats, sizeof(s), hipMemcpyDeviceToHost));
     out->search_distances = s[0];
     out->search_adjacency = s[1];
@@ -1905,6 +1932,7 @@ int vsg_index_stats(const vsg_index_t* h, vsg_stats_t* out) {
     out->build_sort_ns = h->t_sort_ns;
     out->build_reverse_ns = h->t_reverse_ns;
     out->build_select_ns = h->t_select_ns;
+    out->search_filter_overflow = s[16];
     return VSG_OK;
 }
 
@@ -1920,7 +1948,7 @@ extern "C" int vsg_debug_counters(const vsg_index_t* h, uint64_t* out16) {
 int vsg_index_reset_stats(vsg_index_t* h) {
     if (!h) return fail(VSG_EINVAL, "null index");
     DeviceGuard dg(h->device);
-    HIP_TRY(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(h->d_stats, 0, VSG_NSTATS * sizeof(unsigned long long)));
     h->build_vectors = 0;
     h->build_batches = 0;
     h->t_insert_ns = 0;

@@ -40,6 +40,11 @@ struct SearchParams {
     int waves;                  // waves per query: 1 (hnsw_search_kernel), 2 or 4 (cooperative)
     int reg;                    // 1: hnsw_search_reg_kernel (candidate set in VGPRs; ignores waves)
     int upper_ef;               // > 1: level-1 beam of this width seeds level 0 (reg kernel; opt-in)
+    // The index holds removed entries: usearch's filtered base-level search
+    // (index_dense `allow` predicate: removed nodes traversed, never results;
+    // hnsw_search_filt.hip).  removed_frac sizes the candidate set.
+    int filt;
+    float removed_frac;
 };
 
 struct InsertParams {
@@ -141,6 +146,10 @@ struct RerankParams {
     uint32_t* out_counts;
 };
 
+// kernel counter block (d_stats): [0..2] search, [3..9] build, [10..15] wave
+// clocks (tools), [16] filtered-search overflow
+constexpr int VSG_NSTATS = 32;
+
 // key layout of the reverse-link pairs
 constexpr int PAIR_U_BITS = 29;
 constexpr int PAIR_V_SHIFT = 29;
@@ -160,6 +169,8 @@ size_t insert_lds_bytes(int efc, int hash, int m0);
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
 hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
+// filtered search (p.filt): register set when it fits, else the sorted LDS list
+hipError_t launch_search_filt(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
 size_t search_reg_lds_bytes(int hash);
 // split insert: beam kernel then selection kernel (efc <= 192: register beam)
 hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s,

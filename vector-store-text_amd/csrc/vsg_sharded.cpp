@@ -614,6 +614,9 @@ int vsg_sharded_compact(vsg_sharded_t* h, size_t* n_dropped) {
 int vsg_sharded_stats(const vsg_sharded_t* h, vsg_stats_t* out) {
     if (!h || !out) return sfail(VSG_EINVAL, "null argument");
     std::memset(out, 0, sizeof(*out));
+    // counters add up over the shards; the build device times do not -- the
+    // shards build concurrently (one stream per shard), so the sharded index's
+    // build took as long as its slowest shard: the maximum of each
     for (vsg_index_t* s : h->shard) {
         vsg_stats_t t;
         const int rc = vsg_index_stats(s, &t);
@@ -621,6 +624,14 @@ int vsg_sharded_stats(const vsg_sharded_t* h, vsg_stats_t* out) {
         const uint64_t* a = reinterpret_cast<const uint64_t*>(&t);
         uint64_t* b = reinterpret_cast<uint64_t*>(out);
         for (size_t i = 0; i < sizeof(vsg_stats_t) / 8; ++i) b[i] += a[i];
+        out->build_insert_ns -= t.build_insert_ns;
+        out->build_sort_ns -= t.build_sort_ns;
+        out->build_reverse_ns -= t.build_reverse_ns;
+        out->build_select_ns -= t.build_select_ns;
+        out->build_insert_ns = std::max(out->build_insert_ns, t.build_insert_ns);
+        out->build_sort_ns = std::max(out->build_sort_ns, t.build_sort_ns);
+        out->build_reverse_ns = std::max(out->build_reverse_ns, t.build_reverse_ns);
+        out->build_select_ns = std::max(out->build_select_ns, t.build_select_ns);
     }
     return VSG_OK;
 }

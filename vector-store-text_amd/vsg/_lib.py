@@ -69,6 +69,7 @@ class Stats(C.Structure):
         ("build_sort_ns", C.c_uint64),
         ("build_reverse_ns", C.c_uint64),
         ("build_select_ns", C.c_uint64),
+        ("search_filter_overflow", C.c_uint64),
     ]
 
 

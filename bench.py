@@ -82,9 +82,16 @@ def parse():
                     help="experiment: order the query batch by synthetic cluster id")
     ap.add_argument("--sort-base", default="none", choices=("none", "cluster"),
                     help="experiment: insert base rows in synthetic-cluster order (spatial slot ids)")
-    ap.add_argument("--multi", default="both", choices=("both", "shard", "replica"),
-                    help="N>1: row-range shards + all-gather merge (strong) and/or full replicas + query "
-                         "split (weak); 'both' reports the shard leg as value and the replica leg beside it")
+    ap.add_argument("--multi", default="all", choices=("all", "both", "shard", "replica", "hybrid"),
+                    help="N>1 legs: shard = row-range shards over all N GPUs + all-gather merge (strong); "
+                         "replica = full replicas, query split (weak); hybrid = S-GPU row-shard groups x "
+                         "N/S replica groups, each group serving its own batch (weak in groups); "
+                         "all = every leg, the hybrid one as value; both = shard (value) + replica")
+    ap.add_argument("--shards-per-group", type=int, default=2,
+                    help="hybrid leg: GPUs (row shards) per replica group")
+    ap.add_argument("--abi-leg", type=int, default=1,
+                    help="N>1: also time the drop-in's own multi-GPU path -- one vsg_sharded_t over all N "
+                         "devices in rank 0's process (include/vsg.h vsg_sharded_*), peer-DMA gather + HIP merge")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse several ranks on one GPU (collectives via host)")
     return ap.parse_args()
@@ -111,6 +118,14 @@ class Ctx:
             else:
                 dist.init_process_group(a.dist_backend)
         self.stream = torch.cuda.current_stream()
+        self._groups = {}
+
+    def group_of(self, S):
+        """Process group of this rank's row-shard group (ranks [g S, (g+1) S));
+        every rank creates every group, in the same order."""
+        if S not in self._groups:
+            self._groups[S] = [self.dist.new_group(list(range(g * S, (g + 1) * S))) for g in range(self.world // S)]
+        return self._groups[S][self.rank // S]
 
     def barrier(self):
         if self.world > 1:
@@ -139,15 +154,29 @@ def hnsw_leg(c, mode):
     from vsg.distributed import gather_topk, merge_topk
 
     a, world, rank = c.a, c.world, c.rank
-    sharded = mode == "shard"
-    replica = mode == "replica"
+    # shard topology: (position in the row-shard group, its size, its process group)
+    # and the replica group this rank belongs to (each group serves its own batch)
+    if mode == "shard":
+        srank, sworld, pg, grp, ngrp = rank, world, None, 0, 1
+    elif mode == "hybrid":
+        S = max(1, min(a.shards_per_group, world))
+        if world % S:
+            raise SystemExit(f"bench.py: --shards-per-group {S} does not divide {world} ranks")
+        pg = c.group_of(S)
+        srank, sworld, grp, ngrp = rank % S, S, rank // S, world // S
+    elif mode == "replica":
+        srank, sworld, pg, grp, ngrp = 0, 1, None, rank, world
+    else:
+        srank, sworld, pg, grp, ngrp = 0, 1, None, 0, 1
+    sharded = sworld > 1
+    replica = ngrp > 1
     bs, qs, ms = G.config_seeds(a.config)
-    lo, hi = (rank * a.rows // world, (rank + 1) * a.rows // world) if sharded else (0, a.rows)
+    lo, hi = (srank * a.rows // sworld, (srank + 1) * a.rows // sworld) if sharded else (0, a.rows)
     nloc = hi - lo
 
     # inputs in HBM
     x = vsg.datagen_device(a.data, nloc, a.dim, bs, ms, start=lo)
-    q = vsg.datagen_device(a.data, a.queries, a.dim, qs, ms, start=(rank * a.queries if replica else 0))
+    q = vsg.datagen_device(a.data, a.queries, a.dim, qs, ms, start=grp * a.queries)
     qgt = vsg.datagen_device(a.data, a.gt_queries, a.dim, qs, ms, start=0)  # same on every rank
     if a.sort_queries == "cluster":
         cl = (G.splitmix64(G._stream(qs, G.TAG_CLUSTER) + np.arange(a.queries, dtype=np.uint64))
@@ -176,7 +205,7 @@ def hnsw_leg(c, mode):
         del warm
 
     # build (timed; not part of the QPS step)
-    seed = 0x5EED + (rank if sharded else 0)
+    seed = 0x5EED + (srank if sharded else 0)
     index = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 128, device=c.local, seed=seed)
     index.reserve(nloc)
     c.barrier()
@@ -184,14 +213,14 @@ def hnsw_leg(c, mode):
     index.add_device(keys_np, x, stream=c.stream)
     torch.cuda.synchronize()
     build_s = c.max_over_ranks(time.perf_counter() - t0)
-    rows_built = a.rows if sharded else a.rows  # sharded: N shards of rows/N concurrently
+    rows_built = a.rows  # sharded: S shards of rows/S concurrently (every group builds the whole index)
     bstats = index.stats()
 
     def search(qt, ef, ks, exact=False):
         keys, dists = index.search_device(qt, ks, ef, stream=c.stream, exact=exact)
         if not sharded:
             return keys, dists
-        gk, gd = gather_topk(keys, dists)
+        gk, gd = gather_topk(keys, dists, pg)
         return merge_topk(gk, gd, a.k, stream=c.stream)
 
     # ground truth: exact GPU brute force (f32 MFMA), same merge path
@@ -217,7 +246,7 @@ def hnsw_leg(c, mode):
             grid = tuple(e for e in grid if e >= max(16, a.k))
         ef, lo_fail = None, None
         for cand in grid:
-            if sharded and cand * world < a.k:
+            if sharded and cand * sworld < a.k:
                 continue
             r = recall_of(search(qgt, cand, kshard(cand))[0])
             sweep.append((cand, r))
@@ -266,12 +295,12 @@ def hnsw_leg(c, mode):
             keys, dists = index.search_device(q, ks, ef, stream=s)
             evs[i][1].record(s)
             if sharded:
-                gk, gd = gather_topk(keys, dists)
+                gk, gd = gather_topk(keys, dists, pg)
                 keys, dists = merge_topk(gk, gd, a.k, stream=s)
     c.barrier()
     elapsed = c.max_over_ranks(time.perf_counter() - t0)
     kern_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs)
-    queries_done = (world if replica else 1) * a.queries * a.steps
+    queries_done = ngrp * a.queries * a.steps
     st = index.stats()
     alg_bytes = (st["search_distances"] * row_bytes + st["search_adjacency"] * 2 * a.M * 4) / a.steps
     kern_ms_avg = kern_ms / a.steps
@@ -354,7 +383,7 @@ def hnsw_leg(c, mode):
     return {
         "multi_entry": multi,
         "f16_rerank": rerank,
-        "mode": mode, "index": index, "q": q, "x": x, "nloc": nloc,
+        "mode": mode, "index": index, "q": q, "x": x, "nloc": nloc, "shards": sworld, "groups": ngrp,
         "qps": queries_done / elapsed, "ms_per_step": 1000.0 * elapsed / a.steps,
         "ef": ef, "k_shard": ks, "recall": recall, "sweep": sweep,
         "build_s": build_s, "build_vps": rows_built / build_s,
@@ -415,17 +444,30 @@ def main():
             c.dist.destroy_process_group()
         return
 
+    S = max(1, min(a.shards_per_group, world))
+    hybrid_ok = world > 1 and 1 < S < world and world % S == 0
     if world == 1:
         legs = ["single"]
+    elif a.multi == "all":
+        legs = ["replica", "shard"] + (["hybrid"] if hybrid_ok else [])
+    elif a.multi == "both":
+        legs = ["replica", "shard"]
     else:
-        legs = ["replica", "shard"] if a.multi == "both" else [a.multi]
+        legs = [a.multi]
     res = {}
     for m in legs:
         if res:  # free the previous leg's HBM before the next build
             res[list(res)[-1]].pop("index", None)
         res[m] = hnsw_leg(c, m)
-    head = res["shard"] if "shard" in res else res[legs[0]]
-    replica = head["mode"] == "replica"
+    # headline: the hybrid layout (row-shard groups of S GPUs, one replica group per S
+    # GPUs) when it was run, else the pure row-shard leg, else the only leg
+    head = res.get("hybrid") or res.get("shard") or res[legs[0]]
+    replica = head["groups"] > 1
+    parallelism = {"single": "1 GPU",
+                   "shard": f"row-shard x{world} + RCCL all-gather top-k + HIP merge",
+                   "replica": f"replica x{world}, query split ({a.queries} queries/GPU/step)",
+                   "hybrid": f"row-shard x{head['shards']} per group x {head['groups']} replica groups "
+                             f"(RCCL all-gather top-k within a group + HIP merge; {a.queries} queries/group/step)"}
     out = {
         "metric": f"kNN QPS @ recall@10>={a.target_recall} (HNSW, {a.rows} x {a.dim} {a.quant} {a.metric})",
         "value": round(head["qps"], 1),
@@ -437,19 +479,17 @@ def main():
         "higher_is_better": True,
         # N=1 is the first point of the row-shard series the default N>1 run reports
         "scaling": "weak" if (replica or (world == 1 and a.multi == "replica")) else "strong",
+        "layout": {"shards_per_group": head["shards"], "groups": head["groups"]},
         "vs_baseline": None,
         "dtype": a.quant,
         "data": f"synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py), "
-                f"{a.queries} queries/step" + ("/GPU" if replica else ""),
+                f"{a.queries} queries/step" + ("/group" if replica else ""),
         "config": {"workload": f"C{a.config + 1}: {a.rows} x {a.dim} {a.data} f32 input, {a.quant} storage, "
                                f"{a.metric} HNSW M={a.M} efC={a.efc} k={a.k}",
-                   "index_rows": a.rows, "dim": a.dim, "queries_per_step": a.queries * (world if replica else 1),
+                   "index_rows": a.rows, "dim": a.dim, "queries_per_step": a.queries * head["groups"],
                    "ef": head["ef"], "k_shard": head["k_shard"], "recall_at_10": round(head["recall"], 4),
                    "ef_sweep": head["sweep"],
-                   "parallelism": {"single": "1 GPU",
-                                   "shard": f"row-shard x{world} + RCCL all-gather top-k + HIP merge",
-                                   "replica": f"replica x{world}, query split ({a.queries} queries/GPU/step)"}[
-                                       head["mode"]]},
+                   "parallelism": parallelism[head["mode"]]},
         "build_vectors_per_s": round(head["build_vps"], 1),
         "build_seconds": round(head["build_s"], 3),
         "roofline": {"bound": "hbm", "achieved": round(head["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
@@ -467,18 +507,33 @@ def main():
         "f16_traversal_rerank": head.get("f16_rerank"),
         "multi_entry": head.get("multi_entry"),
     }
-    if "replica" in res and head["mode"] != "replica":
-        s = res["replica"]
-        out["replica_mode"] = {"qps": round(s["qps"], 1), "ms_per_step": round(s["ms_per_step"], 3),
-                               "ef": s["ef"], "recall_at_10": round(s["recall"], 4),
-                               "build_vectors_per_s": round(s["build_vps"], 1),
-                               "build_seconds": round(s["build_s"], 3),
-                               "kernel_ms": round(s["kern_ms"], 3),
-                               "dist_evals_per_query": round(s["dist_per_query"], 1),
-                               "queries_per_step": a.queries * world,
-                               "scaling": "weak",
-                               "note": "every rank holds the whole index and serves its own query batch",
-                               "at_config_ef": s["at_config_ef"]}
+    notes = {"replica": "every rank holds the whole index and serves its own query batch",
+             "shard": "every query searched on all N row shards, all-gather + merge (the north star's layout)",
+             "hybrid": "row-shard groups of S GPUs, each group serving its own query batch"}
+    for m, s in res.items():
+        if s is head:
+            continue
+        out[f"{m}_mode"] = {"qps": round(s["qps"], 1), "ms_per_step": round(s["ms_per_step"], 3),
+                            "ef": s["ef"], "k_shard": s["k_shard"], "recall_at_10": round(s["recall"], 4),
+                            "build_vectors_per_s": round(s["build_vps"], 1),
+                            "build_seconds": round(s["build_s"], 3),
+                            "kernel_ms": round(s["kern_ms"], 3),
+                            "dist_evals_per_query": round(s["dist_per_query"], 1),
+                            "queries_per_step": a.queries * s["groups"],
+                            "shards_per_group": s["shards"], "groups": s["groups"],
+                            "parallelism": parallelism[m],
+                            "scaling": "weak" if s["groups"] > 1 else "strong",
+                            "note": notes.get(m, ""),
+                            "at_config_ef": s["at_config_ef"]}
+    # the drop-in's own multi-GPU path (one vsg_sharded_t over all N devices in one
+    # process, as the reference's single process would bind it): rank 0 runs it while
+    # the other ranks wait at a barrier with their HBM freed
+    if world > 1 and a.abi_leg:
+        res[list(res)[-1]].pop("index", None)
+        c.barrier()
+        if rank == 0:
+            out["sharded_abi"] = abi_leg(c)
+        c.barrier()
     # CPU baseline (rank 0, N=1 only): oracle/ restatement of usearch
     if world == 1 and rank == 0 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(a, head["index"], head["q"], head["ef"], head["x"], head["gt"])
@@ -585,22 +640,100 @@ def run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_ove
         print(json.dumps(out), flush=True)
 
 
+def abi_leg(c):
+    """One `vsg_sharded_t` over the node's N devices (include/vsg.h vsg_sharded_*,
+    csrc/vsg_sharded.cpp): keys routed by splitmix64(key) mod N, shards built
+    concurrently (one host thread + stream each), every query searched on every
+    shard, per-shard top-k copied to the answering device by peer DMA (xGMI) and
+    merged there by the HIP merge kernel.  Same data, ef procedure and recall
+    target as the other legs; timed with vsg_sharded_search_device."""
+    import torch
+
+    import vsg
+    from vsg import datagen as G
+
+    a, world = c.a, c.world
+    ndev = max(1, torch.cuda.device_count())
+    devices = [r % ndev for r in range(world)]  # 1 GPU (gloo rehearsal): every shard on device 0
+    bs, qs, ms = G.config_seeds(a.config)
+    idx = vsg.ShardedIndex(a.dim, a.metric, a.quant, a.M, a.efc, 128, devices=devices,
+                           answer_device=c.local, seed=0x5EED)
+    keys = np.arange(a.rows, dtype=np.uint64)
+    CH = 250_000  # host staging in pieces (rows generated in HBM, copied out)
+    xs = [vsg.datagen_device(a.data, min(CH, a.rows - s), a.dim, bs, ms, start=s).cpu().numpy()
+          for s in range(0, a.rows, CH)]
+    x = np.concatenate(xs)
+    del xs
+    idx.reserve(a.rows)
+    t0 = time.perf_counter()
+    idx.add(keys, x)
+    build_s = time.perf_counter() - t0
+    del x
+    q = vsg.datagen_device(a.data, a.queries, a.dim, qs, ms, start=0)
+    qgt = vsg.datagen_device(a.data, a.gt_queries, a.dim, qs, ms, start=0)
+    torch.cuda.synchronize()
+    gt = idx.search_device(qgt, a.k, exact=True, stream=c.stream)[0].cpu().numpy()
+
+    def recall_at(ef):
+        f = idx.search_device(qgt, a.k, ef, stream=c.stream)[0].cpu().numpy()
+        return float((f[:, :, None] == gt[:, None, :]).any(axis=1).sum(axis=1).mean() / a.k)
+
+    sweep, ef, lo_fail = [], None, None
+    for cand in (10, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256, 384, 512):
+        r = recall_at(cand)
+        sweep.append((cand, r))
+        if r >= a.target_recall:
+            ef = cand
+            break
+        lo_fail = cand
+    if ef is None:
+        ef = sweep[-1][0]
+    elif lo_fail is not None:
+        e_lo, e_hi = lo_fail, ef
+        while e_hi - e_lo > 1:
+            mid = (e_lo + e_hi) // 2
+            r = recall_at(mid)
+            sweep.append((mid, r))
+            e_lo, e_hi = (e_lo, mid) if r >= a.target_recall else (mid, e_hi)
+        ef = e_hi
+    for _ in range(max(1, a.warmup)):
+        idx.search_device(q, a.k, ef, stream=c.stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        idx.search_device(q, a.k, ef, stream=c.stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    st = idx.stats()
+    res = {"qps": round(a.queries * a.steps / el, 1), "ms_per_step": round(1000.0 * el / a.steps, 3),
+           "ef": ef, "recall_at_10": round(dict(sweep)[ef], 4), "ef_sweep": sweep,
+           "build_vectors_per_s": round(a.rows / build_s, 1), "build_seconds": round(build_s, 3),
+           "build_device_s_max_shard": round((st["build_insert_ns"] + st["build_sort_ns"] +
+                                              st["build_reverse_ns"]) * 1e-9, 4),
+           "shards": world, "devices": devices, "answer_device": c.local,
+           "shard_rows": [idx.shard(g).size() for g in range(world)],
+           "note": "one process, vsg_sharded_* C ABI over all N devices: host-buffer add (PCIe included in "
+                   "build_seconds), device-resident queries, peer-DMA gather + HIP merge"}
+    idx.close()
+    return res
+
+
 def build_roofline(a, head):
     """The build against the HBM roofline on DEVICE time (HIP events around every
     batch's launches on the build stream, vsg_stats_t.build_*_ns).  Dominant kernel:
-    hnsw_insert_beam_kernel (descent + efC beam; build_insert_ns - build_select_ns).
-    Algorithmic bytes per inserted vector: one row per distance evaluation of the
-    descent and beam (distinct nodes of one wave's traversal) + one level-0
-    adjacency row (M0 x 4 B) per expansion.  Beside it, each with its own line:
-      * hnsw_insert_select_kernel (heuristic neighbour selection): one row per
-        selection distance evaluation -- rows the beam fetched moments before, so
-        mostly L2 / MALL hits (achieved above HBM peak means cache hits);
-      * hnsw_reverse_kernel: one row per distance evaluation of the re-selection
-        (and of recomputed neighbour distances, zero since round 3 stores them
-        beside the adjacency).
-    `traffic` = PMC HBM bytes of the same kernel over the whole build
-    (profiles/build_pmc.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes) when it
-    matches this workload."""
+    hnsw_insert_beam_kernel (descent + efC beam; build_insert_ns - build_select_ns),
+    beside it hnsw_insert_select_kernel (heuristic neighbour selection) and
+    hnsw_reverse_kernel (reverse links), each with its own line.
+
+    `frac` = measured HBM bytes / device time / 8 TB/s: the PMC bytes of the kernel
+    over the whole build (profiles/build_pmc.json -- FETCH_SIZE x2 + WRITE_SIZE,
+    separate rocprofv3 --pmc passes of this workload) over the same kernel's device
+    time; None when no PMC summary of this workload is committed.  It can not
+    exceed 1.  The kernel-counted figure -- one row per distance evaluation, one
+    adjacency row per expansion -- counts rows that co-resident waves share through
+    L2 / MALL once per evaluation, so over the device time it is a cache-credited
+    rate that can exceed the HBM peak (round 3 reported it as `frac`: 1.03 / 2.23 /
+    1.37); it is kept as `alg_gbs_cache_credited` with `alg_over_traffic`."""
     st, rb = head["bstats"], head["row_bytes"]
     sel_ins = st["build_select_distances"]
     sel_rev = st["reverse_select_distances"] + st["reverse_recompute_distances"]
@@ -614,38 +747,33 @@ def build_roofline(a, head):
     try:
         d = json.load(open(os.path.join(ROOT, "profiles", "build_pmc.json")))
         w = d.get("workload", {})
-        if (w.get("n"), w.get("dim"), w.get("metric"), w.get("M"), w.get("efc")) == (
-                head["nloc"], a.dim, a.metric, a.M, a.efc):
+        if (w.get("n"), w.get("dim"), w.get("metric"), w.get("M"), w.get("efc"), w.get("forward_links")) == (
+                head["nloc"], a.dim, a.metric, a.M, a.efc, "M"):
             pmc = d
     except (OSError, ValueError):
         pass
 
-    def tfrac(traffic, t):
-        # measured HBM bytes (PMC) over the same device time: the HBM utilisation itself
-        # (`frac` above 1 = algorithmic bytes served by L2 / MALL, not HBM)
-        return round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None
-
     def line(kernel, alg, t, traffic):
         g = alg / t / 1e9
-        return {"kernel": kernel, "alg_bytes": int(alg), "kernel_s": round(t, 4), "achieved": round(g, 1),
-                "frac": round(g / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_over_alg": round(traffic / alg, 3) if traffic and alg else None,
-                "traffic_frac": tfrac(traffic, t)}
+        return {"kernel": kernel, "kernel_s": round(t, 4),
+                "achieved": round(traffic / t / 1e9, 1) if traffic else None,
+                "frac": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                "traffic": traffic, "alg_bytes": int(alg), "alg_gbs_cache_credited": round(g, 1),
+                "alg_over_traffic": round(alg / traffic, 3) if traffic and alg else None}
 
-    ach = beam_bytes / t_beam / 1e9
-    return {"bound": "hbm", "kernel": "hnsw_insert_beam_kernel", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc.get("beam_hbm_bytes"),
-            "traffic_frac": tfrac(pmc.get("beam_hbm_bytes"), t_beam),
-            "traffic_unit": "HBM bytes over all launches of the kernel in the build",
-            "alg_bytes_insert": int(beam_bytes),
-            "kernel_s": {"beam": round(t_beam, 4), "select": round(ns["select"], 4), "sort": round(ns["sort"], 4),
-                         "reverse": round(ns["reverse"], 4)},
-            "select": line("hnsw_insert_select_kernel", sel_bytes, ns["select"], pmc.get("select_hbm_bytes")),
-            "reverse": line("hnsw_reverse_kernel", rev_bytes, ns["reverse"], pmc.get("reverse_hbm_bytes")),
-            "wall_s": round(head["build_s"], 4),
-            "beam_distance_evals_per_vector": round(beam / max(1, head["nloc"]), 1),
-            "selection_distance_evals_per_vector": round(sel_ins / max(1, head["nloc"]), 1),
-            "reverse_distance_evals_per_vector": round(sel_rev / max(1, head["nloc"]), 1)}
+    out = line("hnsw_insert_beam_kernel", beam_bytes, t_beam, pmc.get("beam_hbm_bytes"))
+    out.update({"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "traffic_unit": "HBM bytes over all launches of the kernel in the build (PMC)",
+                "kernel_s_all": {"beam": round(t_beam, 4), "select": round(ns["select"], 4),
+                                 "sort": round(ns["sort"], 4), "reverse": round(ns["reverse"], 4)},
+                "select": line("hnsw_insert_select_kernel", sel_bytes, ns["select"], pmc.get("select_hbm_bytes")),
+                "reverse": line("hnsw_reverse_kernel", rev_bytes, ns["reverse"], pmc.get("reverse_hbm_bytes")),
+                "wall_s": round(head["build_s"], 4),
+                "beam_distance_evals_per_vector": round(beam / max(1, head["nloc"]), 1),
+                "selection_distance_evals_per_vector": round(sel_ins / max(1, head["nloc"]), 1),
+                "reverse_distance_evals_per_vector": round(sel_rev / max(1, head["nloc"]), 1),
+                "reverse_prunes": st["reverse_prunes"], "reverse_appends": st["reverse_appends"]})
+    return out
 
 
 def pmc_traffic(a, ef):
@@ -659,8 +787,10 @@ def pmc_traffic(a, ef):
     except (OSError, ValueError):
         return None
     w = d.get("workload", {})
-    if (w.get("n"), w.get("dim"), w.get("queries"), w.get("ef"), w.get("metric")) != (
-            a.rows, a.dim, a.queries, ef, a.metric):
+    # forward_links "M": a graph built with usearch's <= M forward links per level
+    # (round 4); earlier summaries profiled the M0-forward graph
+    if (w.get("n"), w.get("dim"), w.get("queries"), w.get("ef"), w.get("metric"), w.get("forward_links")) != (
+            a.rows, a.dim, a.queries, ef, a.metric, "M"):
         return None
     return d.get("hbm_bytes_per_launch")
 

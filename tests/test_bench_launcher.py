@@ -38,3 +38,31 @@ def test_gpus_2_launches_two_ranks():
     assert r["config"]["parallelism"].startswith("row-shard x2")
     assert r["config"]["recall_at_10"] >= 0.95
     assert r["replica_mode"]["queries_per_step"] == 4000
+    # the drop-in's own multi-GPU path (one vsg_sharded_t over both "devices" in rank 0)
+    abi = r["sharded_abi"]
+    assert abi["shards"] == 2 and abi["devices"] == [0, 0] and sum(abi["shard_rows"]) == 100000
+    assert abi["recall_at_10"] >= 0.95 and abi["qps"] > 0 and abi["build_vectors_per_s"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_gpus_4_hybrid_layout():
+    """Four gloo ranks on the one GPU: the headline is the hybrid layout (2 row shards per
+    group x 2 replica groups, all-gather inside a group), with the pure row-shard, replica
+    and sharded-ABI legs beside it."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "4", "--dist-backend", "gloo",
+                          "--rows", "60000", "--queries", "1000", "--gt-queries", "1000", "--steps", "2",
+                          "--warmup", "1", "--config-ef", "0", "--upper-ef", "0", "--rerank-leg", "0", "--no-cpu",
+                          "--warm-build", "0"],
+                         env=env, capture_output=True, text=True, timeout=840, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [json.loads(s) for s in out.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = lines[0]
+    assert r["n_gpus"] == 4 and r["layout"] == {"shards_per_group": 2, "groups": 2}
+    assert r["scaling"] == "weak" and r["config"]["queries_per_step"] == 2000
+    assert r["config"]["recall_at_10"] >= 0.95
+    assert r["shard_mode"]["shards_per_group"] == 4 and r["shard_mode"]["queries_per_step"] == 1000
+    assert r["replica_mode"]["groups"] == 4 and r["replica_mode"]["queries_per_step"] == 4000
+    assert r["sharded_abi"]["shards"] == 4

@@ -69,3 +69,30 @@ def test_rust_call_sequence_on_gpu():
     out = subprocess.run([exe], capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.strip().endswith("ok")
+
+
+ROUTES = os.path.join(ROOT, "rust", "src", "httproutes_vector.rs")
+
+
+def test_rust_vector_routes_match_client_and_python_twin():
+    """rust/src/httproutes_vector.rs (source only) serves the client shape of
+    /root/reference/tests/integration/httpclient.rs:35-80 with the same paths, request /
+    response fields and status mapping as vsg/httproutes.py (which the HTTP tests run)."""
+    from vsg import httproutes as H
+    src = open(ROUTES).read()
+    pairs = re.findall(r'\.route\("([^"]+)",\s*(get|post)\(', src)
+    assert pairs == [("/api/v1/indexes", "get"), ("/api/v1/indexes/{keyspace}/{index}/ann", "post"),
+                     ("/api/v1/indexes/{keyspace}/{index}/count", "get")]
+    assert H.API == "/api/v1"
+    req = re.search(r"pub struct PostIndexAnnRequest \{(.*?)\n\}", src, re.S).group(1)
+    assert re.findall(r"pub (\w+):", req) == ["embedding", "limit"]
+    assert "#[serde(default)]\n    pub limit: Limit" in req      # missing limit -> 1 (Limit::default)
+    resp = re.search(r"pub struct PostIndexAnnResponse \{(.*?)\n\}", src, re.S).group(1)
+    assert re.findall(r"pub (\w+):", resp) == ["primary_keys", "distances"]
+    assert set(H.ann_response(["pk"], [1], [0.5])) == {"primary_keys", "distances"}
+    # statuses: unknown index 404 with an empty body, index errors 500 with the error text
+    assert src.count('(StatusCode::NOT_FOUND, "")') == 3
+    assert 'format!("index.ann request error: {err}")' in src
+    assert 'format!("index.count request error: {err}")' in src
+    assert "engine.get_index(" in src and "actor.ann(request.embedding, request.limit)" in src
+    assert "actor.count()" in src and "engine.get_index_ids()" in src

@@ -50,7 +50,9 @@ def search(fdir, wdir, n, dim, nq, ef, metric, path=None):
     fetch_kib = sum(fv[k] for k in full) / len(full)
     write_kib = sum(wv[k] for k in fullw) / max(1, len(fullw))
     out = {
-        "workload": {"n": int(n), "dim": int(dim), "queries": nq, "ef": int(ef), "metric": metric},
+        # forward_links "M": usearch's <= M forward links per level (round 4 on)
+        "workload": {"n": int(n), "dim": int(dim), "queries": nq, "ef": int(ef), "metric": metric,
+                     "forward_links": "M"},
         "kernel": "hnsw_search_reg_kernel",
         "dispatches": len(full),
         "fetch_size_kib_raw": round(fetch_kib, 1),
@@ -63,7 +65,8 @@ def search(fdir, wdir, n, dim, nq, ef, metric, path=None):
 
 
 def build(fdir, wdir, n, dim, metric, M, efc, path=None):
-    out = {"workload": {"n": int(n), "dim": int(dim), "metric": metric, "M": int(M), "efc": int(efc)},
+    out = {"workload": {"n": int(n), "dim": int(dim), "metric": metric, "M": int(M), "efc": int(efc),
+                        "forward_links": "M"},
            "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes; summed over every "
                          "dispatch of the kernel in ONE build (the probe builds once per process)"}
     # "hnsw_insert_": the fused insert kernel or both launches of the split insert

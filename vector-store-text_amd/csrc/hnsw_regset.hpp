@@ -379,15 +379,24 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
 // of B at or below the radius are exactly usearch's unexpanded `next` entries at
 // or below it -- an over-admitted removed key lies beyond the radius forever --
 // so both expand the same node or both stop.  Compaction keeps the ef smallest
-// live keys and every key below the ef-th; expanded removed keys carry no
-// state (a forgotten id evaluated again only repeats an expansion whose
-// candidates are all known) and are dropped first.
+// live keys and every key at or below the ef-th, expanded or not: an expanded
+// removed key stays in B so that a forgotten id evaluated again is recognised
+// (B.contains) and never expanded twice -- which also bounds the traversal.
+// A key dropped by compaction lies above tkey and is never admitted again.
+//
+// Room: B must hold the ef live keys and the removed ones at or below the
+// radius; the row class is sized from the index's removed fraction for that.
+// If it still runs out, the query degrades (counted in F.overflow): every
+// removed key leaves B and no removed candidate is admitted any more -- the
+// classic live-only traversal, which terminates; its results are well-formed
+// but no longer usearch's exactly.
 struct FiltState {
     uint32_t remm;     // bit r: slot r of this lane holds a removed node
     int nlive;         // live keys in B (wave-uniform)
     uint64_t maxlive;  // largest live key in B while nlive < ef
     uint64_t rad0;     // the start's key: the radius while no live key is admitted
-    uint32_t overflow; // candidates / keys dropped for want of room (0 in the tests)
+    uint32_t overflow; // keys / candidates dropped for want of room (0 in the tests)
+    bool degraded;     // out of room once: removed nodes are no longer admitted
 };
 
 __device__ __forceinline__ uint64_t wave_max64(uint64_t v) { return ~wave_min64(~v); }
@@ -414,13 +423,9 @@ template <int R> __device__ __forceinline__ void recount(RegSet<R>& B, FiltState
     B.size = c;
 }
 
-// Make room in B: expanded removed keys go; with >= ef live keys, every key
-// beyond the ef-th live key goes (tkey = that key, the radius).
+// Make room in B: with >= ef live keys, every key beyond the ef-th live key
+// goes (tkey = that key, the radius).
 template <int R> __device__ __forceinline__ void compact_filt(RegSet<R>& B, FiltState& F, int ef) {
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if ((F.remm & B.expm) >> r & 1u) B.k[r] = VSG_KEY_EMPTY;
-    recount(B, F);
     if (F.nlive >= ef) {
         B.compact(ef, F.remm);  // drops keys above the cut; recounts the size
         F.nlive = ef;
@@ -457,7 +462,7 @@ __device__ __forceinline__ void admit_filt(RegSet<R>& B, FiltState& F, bool mine
     const int lane = lane_id();
     // |top| < ef admits everything (tkey is open until a compaction with >= ef
     // live keys sets it to the radius; it only over-admits)
-    bool valid = mine && ck < B.tkey;
+    bool valid = mine && ck < B.tkey && !(F.degraded && rem);
     uint64_t vm = __ballot(valid);
     if (lossy && vm) {
         for (uint64_t mm = vm; mm; mm &= mm - 1) {
@@ -473,23 +478,20 @@ __device__ __forceinline__ void admit_filt(RegSet<R>& B, FiltState& F, bool mine
         vm = __ballot(valid);
         nc = popc64(vm);
         if (B.size + nc > 64 * R) {
-            // No room even so: more removed nodes pending than the set holds.
-            // Drop (and count) the removed keys of B, then removed candidates --
-            // the register class is sized from the index's removed fraction so
-            // that this does not happen (stats[13]; 0 in every test).
+            // No room even so: degrade (see FiltState).  Every removed key leaves
+            // B and removed candidates are refused from now on; the live keys
+            // (< ef, or ef after the compaction) and this batch's live candidates
+            // fit in 64 R >= ef + 64 slots.
             const uint64_t before = (uint64_t)B.size;
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if ((F.remm >> r) & 1u) B.k[r] = VSG_KEY_EMPTY;
             recount(B, F);
-            F.overflow += (uint32_t)(before - (uint64_t)B.size);
-            if (B.size + nc > 64 * R) {
-                const bool drop = valid && rem;
-                F.overflow += (uint32_t)popc64(__ballot(drop));
-                valid = valid && !rem;
-                vm = __ballot(valid);
-                nc = popc64(vm);
-            }
+            F.overflow += (uint32_t)(before - (uint64_t)B.size) + (uint32_t)popc64(__ballot(valid && rem));
+            F.degraded = true;
+            valid = valid && !rem;
+            vm = __ballot(valid);
+            nc = popc64(vm);
         }
     }
     if (nc) {
@@ -521,6 +523,7 @@ __device__ __forceinline__ void beam_reg_filt(const GraphDev& g, const QReg<G, V
     w.vis.clear();
     F.remm = 0;
     F.overflow = 0;
+    F.degraded = false;
     if (ep != VSG_EMPTY) {
         if (lane == 0) {
             bool unrec;

@@ -17,9 +17,11 @@
 //   hnsw_search_filt_kernel      -- sorted LDS list holding live and removed
 //       entries (VSG_REM_BIT), cut at the ef-th live entry; ef up to MAX_EF or
 //       when the register set would be too small.
-// Both count candidates they had to drop for want of room in stats[16]
-// (vsg_stats_t.search_filter_overflow, 0 in every test): exactness holds
-// while that counter stays 0.
+// Both count entries they had to drop for want of room in stats[16]
+// (vsg_stats_t.search_filter_overflow, 0 at the sizes the index's removed
+// fraction selects in every test): exactness holds while that counter stays 0;
+// past it a query degrades to the live-only traversal (hnsw_regset.hpp
+// FiltState), which always terminates.
 #include <hip/hip_runtime.h>
 
 #include "hnsw_common.hpp"
@@ -132,6 +134,7 @@ __device__ void beam_level_filt(const GraphDev& g, const QReg<G, VM, T>& q, cons
     }
     int nlive = r0 ? 0 : 1;
     int lastlive = r0 ? -1 : 0;
+    bool degraded = false;  // out of room once (see below)
     wave_sync();
     int hint = 0;
     for (;;) {
@@ -167,8 +170,8 @@ __device__ void beam_level_filt(const GraphDev& g, const QReg<G, VM, T>& q, cons
                 rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
                 wave_sync();
                 ndist += (uint64_t)cnt;
-                bool valid = lane < cnt;
-                const float cd = valid ? w.tdist[lane] : 0.f;
+                bool valid = lane < cnt && !(degraded && (cfl & 1));
+                const float cd = lane < cnt ? w.tdist[lane] : 0.f;
                 wave_sync();
                 if (valid && nlive >= ef) {  // a full `top`: below the radius only
                     const float rd = L.D()[L.size - 1];
@@ -176,7 +179,7 @@ __device__ void beam_level_filt(const GraphDev& g, const QReg<G, VM, T>& q, cons
                     valid = cand_less(cd, cid, rd, ri);
                 }
                 const int nc = popc64(__ballot(valid));
-                if (nc && L.size + nc > L.cap) overflow += (uint32_t)(L.size + nc - L.cap);
+                const int lost = max(0, L.size + nc - L.cap);  // the largest entries, when the list is full
                 hint = min(hint, L.merge(valid, cd, cid, lossy, w.sd, w.si, (cfl & 1) ? VSG_REM_BIT : 0u));
                 // recount the live entries; cut after the ef-th
                 int nl = 0, last = -1, cut = -1;
@@ -193,11 +196,44 @@ __device__ void beam_level_filt(const GraphDev& g, const QReg<G, VM, T>& q, cons
                     nl += c;
                 }
                 if (cut >= 0) {
+                    // entries a full list dropped lay beyond the radius: never needed
                     L.size = cut + 1;
                     nlive = ef;
                 } else {
                     nlive = nl;
                     lastlive = last;
+                    if (lost) {
+                        // Out of room before ef live entries: degrade (counted).  Every
+                        // removed entry leaves the list and removed candidates are
+                        // refused from now on -- the live-only traversal, which
+                        // terminates.  (Entries are never dropped otherwise: an expanded
+                        // removed one must stay to recognise a forgotten id evaluated
+                        // again, so no node is expanded twice.)
+                        overflow += (uint32_t)lost;
+                        degraded = true;
+                        const float* dd = L.D();
+                        const uint32_t* ii = L.I();
+                        float* nd = L.Dn();
+                        uint32_t* ni = L.In();
+                        int n2 = 0;
+                        for (int r = 0; r < L.size; r += 64) {
+                            const int i = r + lane;
+                            const uint32_t e = i < L.size ? ii[i] : VSG_REM_BIT;
+                            const bool keep = !(e & VSG_REM_BIT);
+                            const uint64_t km = __ballot(keep);
+                            if (keep) {
+                                nd[n2 + lanes_below(km)] = dd[i];
+                                ni[n2 + lanes_below(km)] = e;
+                            }
+                            n2 += popc64(km);
+                        }
+                        overflow += (uint32_t)(L.size - n2);
+                        wave_sync();
+                        L.size = n2;
+                        L.cur ^= 1;
+                        lastlive = n2 - 1;
+                        hint = 0;
+                    }
                 }
             }
             if (!full) break;
@@ -302,9 +338,15 @@ hipError_t launch_search_filt(Storage st, MetricKind mk, const SearchParams& p, 
         else dispatch_all<true>(st, mk, p.g.nchunks, body);
         return err;
     }
-    // sorted LDS list: 16 B per entry, at most MAX_EF entries
-    const int cap = std::min<int>((int)MAX_EF, std::max(p.ef + 64, 2 * need));
-    const size_t lds = wave_lds_bytes(p.hash_size, cap, 0);
+    // sorted LDS list: 16 B per entry, up to 8,192 entries (ef <= MAX_EF live ones and
+    // the removed ones beside them); the visited table gives way to the list within the
+    // 160 KB of LDS a workgroup may hold (a smaller table forgets more: more distance
+    // evaluations, the same results)
+    const int cap = std::min(8192, std::max(p.ef + 64, 2 * need));
+    SearchParams pl = p;
+    const int hmax = (int)(((160 * 1024) - (size_t)cap * 16 - 64 * 16 - 1024) / 4) & ~63;
+    pl.hash_size = std::max(1024, std::min(p.hash_size, hmax));
+    const size_t lds = wave_lds_bytes(pl.hash_size, cap, 0);
     dispatch_all<true>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
         using T = typename decltype(tt)::T;
@@ -313,7 +355,7 @@ hipError_t launch_search_filt(Storage st, MetricKind mk, const SearchParams& p, 
         if (lds > 65536)
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         for (int off = 0; off < p.nq && err == hipSuccess; off += CH) {
-            SearchParams c = p;
+            SearchParams c = pl;
             c.nq = min(CH, p.nq - off);
             c.queries = p.queries + (size_t)off * p.g.row_bytes;
             c.out_keys = p.out_keys + (size_t)off * p.k;

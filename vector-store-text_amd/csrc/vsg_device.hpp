@@ -467,7 +467,8 @@ struct Visited {
 };
 
 // ------------------------------------------------------------- sorted list --
-// (distance, slot) ascending; slot high bit = "expanded".  cap <= MAX_EF (4096).
+// (distance, slot) ascending; slot high bit = "expanded", bit 30 = removed node
+// (filtered search).  cap <= MAX_EF (4096), 8192 for the filtered search.
 
 struct List {
     float* d0;

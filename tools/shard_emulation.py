@@ -9,6 +9,10 @@ is NOT emulated: the all-gather itself (B x k x 12 B per rank, latency-bound).
 Reports per ef: merged recall@10 vs exact ground truth (exact per shard +
 merge), per-shard search time for the whole query batch, the projected G-GPU
 QPS = B / max shard time, and the measured 1-GPU QPS = B / sum of shard times.
+Hybrid layouts (round 4): on --gpus-total T GPUs, T / G replica groups of these
+G row shards each serve their own batch -> projected T-GPU QPS = (T / G) x the
+G-shard QPS; the build of each group is the G-shard build (every group holds the
+whole index).
 
 usage: python tools/shard_emulation.py --rows 100000000 --dim 128 --quant f16 --metric l2sq --data sift --config 3
 """
@@ -39,6 +43,7 @@ def main():
     ap.add_argument("--efs", default="16,32,64,96,128,192,256")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--out", default="gpurun_out/shard_emulation.jsonl")
+    ap.add_argument("--gpus-total", type=int, default=8, help="hybrid projection: GPUs of the node")
     a = ap.parse_args()
 
     import torch
@@ -114,6 +119,11 @@ def main():
                 "dist_evals_per_query_per_shard": dpq, "alg_gbs_per_shard": gbs,
                 "qps_projected_gpus": round(a.queries / max(per), 1),
                 "qps_1gpu_all_shards": round(a.queries / t_all, 1)}
+        if a.gpus_total % G_ == 0:
+            grp = a.gpus_total // G_
+            line["hybrid_projection"] = {"gpus": a.gpus_total, "shards_per_group": G_, "groups": grp,
+                                         "qps": round(grp * a.queries / max(per), 1),
+                                         "build_vectors_per_s": round(a.rows / max(build_s), 1)}
         with open(a.out, "a") as f:
             f.write(json.dumps(line) + "\n")
         print(json.dumps(line), flush=True)

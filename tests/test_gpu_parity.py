@@ -637,3 +637,36 @@ def test_shape96_rows_bitexact(metric, dim, quant, monkeypatch):
         np.testing.assert_array_equal(m.counts, hc)
         np.testing.assert_array_equal(m.keys, hk)
         np.testing.assert_array_equal(m.distances, hd)
+
+
+@pytest.mark.parametrize("metric,dim", [("ip", 64), ("l2sq", 96)])
+def test_exact_only_ktile_mfma_bitexact(metric, dim, monkeypatch):
+    """Exact-only f32 indexes stream the MFMA tiles from a K-tiled copy of the rows
+    (256-row tiles stored stage-major, kept current by every add): bit-exact vs the
+    oracle and vs the row-major loads (VSG_EXACT_KTILE=0), across ragged tiles, appends
+    that land inside a partial tile, tombstones and a compaction."""
+    scale = 16.0 if metric == "ip" else 1.0
+    x = G.uint8_valued(3000, dim, 301) / scale
+    q = G.uint8_valued(70, dim, 302) / scale
+    idx = vsg.Index(dim, metric, exact_only=True)
+    keys = np.arange(3000, dtype=np.uint64) * 5 + 1
+    idx.add(keys[:1000], x[:1000])
+    idx.add(keys[1000:1777], x[1000:1777])     # ends inside a 256-row tile
+    idx.add(keys[1777:], x[1777:])
+    idx.remove(keys[::9])
+    removed = np.zeros(3000, np.uint8)
+    removed[::9] = 1
+
+    def check():
+        ok, od, oc = O.exact_search(metric, x, q, 10, keys=keys, removed=removed)
+        for kt in ("1", "0"):
+            monkeypatch.setenv("VSG_EXACT_KTILE", kt)
+            m = idx.exact_search(q, 10)
+            np.testing.assert_array_equal(m.keys, ok, err_msg=f"ktile={kt}")
+            np.testing.assert_array_equal(m.distances, od, err_msg=f"ktile={kt}")
+            np.testing.assert_array_equal(m.counts, oc)
+        monkeypatch.delenv("VSG_EXACT_KTILE")
+
+    check()
+    assert idx.compact() == len(keys[::9])   # rows move: the copy is rebuilt by the next search
+    check()

@@ -128,16 +128,21 @@ __global__ __launch_bounds__(64 * WQ * WR, 2) void mfma_exact_kernel(MfmaExactPa
         // piece stays live across the K loop (the 64-query tile spilled with them).
         const int xlast = (int)min((size_t)(BR - 1), p.nslots - 1 - r0);
         const int qlast = min(BQ - 1, p.nq - 1 - q0);
+        // base rows: row-major (stride row_floats) or the K-tiled copy, where the
+        // stage's rows are consecutive 128-B rows of one contiguous block
+        const bool kt = p.ktile != nullptr;
+        const uint32_t xstride = kt ? (uint32_t)KT : (uint32_t)p.row_floats;
         auto load_stage = [&](int s, float* xs) {
             const int k0 = s * KT;
             float* qs = xs + BR * LDK;
-            const float* xb = p.vecs + r0 * p.row_floats + k0;
+            const float* xb = kt ? p.ktile + (((r0 / KTILE_ROWS) * (size_t)nst + s) * KTILE_ROWS + r0 % KTILE_ROWS) * KT
+                                 : p.vecs + r0 * p.row_floats + k0;
             const float* qb = p.queries + (size_t)q0 * p.row_floats + k0;
 #pragma unroll
             for (int u = 0; u < BR / 8 / NW; ++u) {
                 const int piece = w * (BR / 8 / NW) + u;
                 const int R = piece * 8 + prow;
-                const uint32_t off = (uint32_t)min(R, xlast) * (uint32_t)p.row_floats + (uint32_t)swz(R, pslot) * 4;
+                const uint32_t off = (uint32_t)min(R, xlast) * xstride + (uint32_t)swz(R, pslot) * 4;
                 __builtin_amdgcn_global_load_lds((gptr_t)(xb + off), (lptr_t)(xs + piece * 8 * LDK), 16, 0, 0);
             }
 #pragma unroll
@@ -225,6 +230,30 @@ __global__ __launch_bounds__(64 * WQ * WR, 2) void mfma_exact_kernel(MfmaExactPa
             p.part_i[o + t] = ld[b][t] < __builtin_inff() ? li[b][t] : VSG_EMPTY;
         }
     }
+}
+
+// one work-item per 16-B chunk of a row: chunk c of row r goes to stage c / 8,
+// slot c % 8 of row r % 256 in tile r / 256
+__global__ __launch_bounds__(256) void ktile_rows_kernel(const float* __restrict__ vecs, int row_floats, size_t r0,
+                                                          size_t r1, float* __restrict__ ktile) {
+    const int nc = row_floats / 4, nst = row_floats / KT;
+    const size_t tot = (r1 - r0) * (size_t)nc;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = r0 + i / nc;
+        const int c = (int)(i % nc);
+        const float4 v = *reinterpret_cast<const float4*>(vecs + r * row_floats + (size_t)c * 4);
+        const size_t o = (((r / KTILE_ROWS) * (size_t)nst + c / 8) * KTILE_ROWS + r % KTILE_ROWS) * KT + (c % 8) * 4;
+        *reinterpret_cast<float4*>(ktile + o) = v;
+    }
+}
+
+hipError_t launch_ktile_rows(const float* vecs, int row_floats, size_t r0, size_t r1, float* ktile, hipStream_t s) {
+    if (r1 <= r0) return hipSuccess;
+    if (row_floats % KT) return hipErrorInvalidValue;
+    const size_t tot = (r1 - r0) * (size_t)(row_floats / 4);
+    const unsigned grid = (unsigned)std::min<size_t>((tot + 255) / 256, 1u << 20);
+    hipLaunchKernelGGL(ktile_rows_kernel, dim3(grid), dim3(256), 0, s, vecs, row_floats, r0, r1, ktile);
+    return hipGetLastError();
 }
 
 hipError_t launch_mfma_exact(MetricKind mk, const MfmaExactParams& p, hipStream_t s) {

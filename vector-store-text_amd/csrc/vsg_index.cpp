@@ -293,6 +293,14 @@ struct vsg_index {
     uint8_t* d_vecs16 = nullptr;
     size_t shadow_cap = 0, shadow_rows = 0, row_bytes16 = 0;
     uint64_t shadow_gen = ~0ull;
+    // K-tiled copy of the f32 rows for the MFMA brute force of exact-only indexes
+    // (MfmaExactParams::ktile): rows [0, ktile_rows) current for ktile_gen; kept up to
+    // date by every add (ensure_ktile before publish) and, after rows move, by the
+    // next exact search
+    std::mutex ktile_mu;
+    float* d_ktile = nullptr;
+    size_t ktile_cap = 0, ktile_rows = 0;
+    uint64_t ktile_gen = ~0ull;
     unsigned long long* d_stats = nullptr;  // [0..2] search, [3..4] build
 
     std::vector<int8_t> h_levels;
@@ -388,6 +396,7 @@ static void free_dev(vsg_index* h) {
     hipFree(h->d_rm);
     hipFree(h->d_vecs);
     hipFree(h->d_vecs16);
+    hipFree(h->d_ktile);
     hipFree(h->d_adj0);
     hipFree(h->d_upper_off);
     hipFree(h->d_upper);
@@ -1276,6 +1285,9 @@ static int put_rows(vsg_index_t* h, const float* vecs, size_t n, bool device_src
     return VSG_OK;
 }
 
+static bool ktile_on(const vsg_index* h);
+static int ensure_ktile(vsg_index* h, size_t slots, hipStream_t s);
+
 // usearch::Index::add (src/index/usearch.rs:221), batched.  Stage under the
 // exclusive lock, write rows and build the graph with no lock held (searches run
 // beside it, VERDICT r1 missing #1), publish under the exclusive lock.
@@ -1326,6 +1338,13 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
         (void)hipStreamSynchronize(h->stream);
         publish(h);
         g_last_error = msg;
+        return rc;
+    }
+    // exact-only f32: the K-tiled MFMA copy of the new rows is part of the add
+    if (ktile_on(h) && (rc = ensure_ktile(h, h->slots, h->stream))) {
+        // rows are in, the copy is not: the next exact search completes it (ktile_rows)
+        h->live += n;
+        publish(h);
         return rc;
     }
     h->live += n;
@@ -1464,6 +1483,45 @@ static int ensure_shadow(vsg_index* h, hipStream_t s) {
     return VSG_OK;
 }
 
+// The K-tiled MFMA copy applies to exact-only f32 indexes whose rows are whole
+// 32-dim stages (VSG_EXACT_KTILE=0: the row-major MFMA loads, probes).
+static bool ktile_on(const vsg_index* h) {
+    return (h->opt.flags & VSG_FLAG_EXACT_ONLY) && h->st == ST_F32 && (h->row_bytes / 4) % 32 == 0 &&
+           env_double("VSG_EXACT_KTILE", 1) != 0;
+}
+
+// Bring the K-tiled copy up to `slots` rows (append-only between vec_gen bumps, as the
+// f16 copy).  Callers: every add before it publishes (rows [0, slots) written), and
+// exact searches (holding h->mu shared) for rows moved by a compaction / import /
+// load.  A reallocation happens only here, under ktile_mu, after a capacity growth
+// that drained every earlier search: a search reads the copy only after its own
+// ensure_ktile returned.
+static int ensure_ktile(vsg_index* h, size_t slots, hipStream_t s) {
+    std::lock_guard<std::mutex> g(h->ktile_mu);
+    const size_t want_cap = (h->cap + KTILE_ROWS - 1) / KTILE_ROWS * KTILE_ROWS;
+    if (h->ktile_gen != h->vec_gen || h->ktile_cap < want_cap || h->ktile_rows > slots) {
+        if (h->ktile_cap < want_cap) {
+            h->fence.drain();
+            hipFree(h->d_ktile);
+            h->d_ktile = nullptr;
+            h->ktile_cap = 0;
+            HIP_TRY(dev_alloc(&h->d_ktile, want_cap * (h->row_bytes / 4)));
+            // padding rows of the last tile are read (clamped loads never, but keep them defined)
+            HIP_TRY(hipMemsetAsync(h->d_ktile, 0, want_cap * h->row_bytes, s));
+            h->ktile_cap = want_cap;
+        }
+        h->ktile_rows = 0;
+        h->ktile_gen = h->vec_gen;
+    }
+    if (h->ktile_rows < slots) {
+        HIP_TRY(launch_ktile_rows(reinterpret_cast<const float*>(h->d_vecs), (int)(h->row_bytes / 4), h->ktile_rows,
+                                  slots, h->d_ktile, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        h->ktile_rows = slots;
+    }
+    return VSG_OK;
+}
+
 static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, size_t k, size_t ef,
                                 uint64_t* ok, float* od, uint32_t* oc, hipStream_t s, bool exact) {
     if (k == 0) return fail(VSG_EINVAL, "k must be >= 1 (Limit is NonZeroUsize)");
@@ -1564,6 +1622,14 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
     if (err == hipSuccess && use_mfma) {
         MfmaExactParams mp{};
         mp.vecs = reinterpret_cast<const float*>(h->d_vecs);
+        if (ktile_on(h)) {
+            const int rk = ensure_ktile(h, slots, s);
+            if (rk) {
+                ws_release(h, ws, s);
+                return rk;
+            }
+            mp.ktile = h->d_ktile;
+        }
         mp.sqnorm = h->d_sqnorm;
         mp.queries = reinterpret_cast<const float*>(qp);
         mp.qsqnorm = qsq;

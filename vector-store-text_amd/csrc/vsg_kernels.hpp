@@ -113,6 +113,12 @@ struct MfmaExactParams {
     int br;                 // base rows per tile: 128 with bq 128, 256 with bq 64
     float* part_d;
     uint32_t* part_i;
+    // K-tiled copy of `vecs` (exact-only f32 indexes; nullptr: row-major `vecs`):
+    // 256-row tiles, each stored stage-major -- [tile][K stage of 32 dims][256 rows][32
+    // floats] -- so one K stage of a row tile is one contiguous block (32 KiB for 256
+    // rows; a 128-row tile reads half of one) instead of 128-B pieces of 256 rows
+    // 4-6 KiB apart.
+    const float* ktile;
 };
 
 struct MergeParams {
@@ -186,6 +192,11 @@ hipError_t launch_rerank(MetricKind mk, const RerankParams& p, hipStream_t s);
 // f32 image rows [r0, r1) -> f16 traversal copy (row_bytes16 stride, padding zeroed)
 hipError_t launch_shadow_f16(const uint8_t* vecs, size_t row_bytes, size_t r0, size_t r1, int dim,
                              uint8_t* out, size_t row_bytes16, hipStream_t s);
+// rows [r0, r1) of row-major f32 `vecs` (row_floats % 32 == 0) -> the K-tiled layout
+// of MfmaExactParams::ktile
+hipError_t launch_ktile_rows(const float* vecs, int row_floats, size_t r0, size_t r1, float* ktile,
+                             hipStream_t s);
+constexpr int KTILE_ROWS = 256;
 // returns hipErrorNotSupported when the MFMA path does not apply (k > 32)
 hipError_t launch_mfma_exact(MetricKind mk, const MfmaExactParams& p, hipStream_t s);
 constexpr int MFMA_BQ = 128, MFMA_BR = 128;

@@ -647,7 +647,7 @@ def test_exact_only_ktile_mfma_bitexact(metric, dim, monkeypatch):
     that land inside a partial tile, tombstones and a compaction."""
     scale = 16.0 if metric == "ip" else 1.0
     x = G.uint8_valued(3000, dim, 301) / scale
-    q = G.uint8_valued(70, dim, 302) / scale
+    q = G.uint8_valued(50, dim, 302) / scale  # <= 64 queries: the 256 x 64 tile
     idx = vsg.Index(dim, metric, exact_only=True)
     keys = np.arange(3000, dtype=np.uint64) * 5 + 1
     idx.add(keys[:1000], x[:1000])
@@ -665,6 +665,9 @@ def test_exact_only_ktile_mfma_bitexact(metric, dim, monkeypatch):
             np.testing.assert_array_equal(m.keys, ok, err_msg=f"ktile={kt}")
             np.testing.assert_array_equal(m.distances, od, err_msg=f"ktile={kt}")
             np.testing.assert_array_equal(m.counts, oc)
+        m = idx.exact_search(np.concatenate([q, q]), 10)  # 100 queries: the 128 x 128 tile
+        np.testing.assert_array_equal(m.keys[:50], ok)
+        np.testing.assert_array_equal(m.distances[50:], od)
         monkeypatch.delenv("VSG_EXACT_KTILE")
 
     check()

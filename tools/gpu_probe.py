@@ -35,7 +35,7 @@ KNOBS = {"frac": "VSG_BUILD_BATCH_FRAC", "max": "VSG_BUILD_BATCH_MAX", "frac2": 
          "hash": "VSG_SEARCH_HASH_FACTOR", "xcd": "VSG_SEARCH_XCD_MAP", "upper": "VSG_SEARCH_UPPER_EF",
          "loc": "VSG_BUILD_LOCALITY", "locmin": "VSG_BUILD_LOCALITY_MIN",
          "piv": "VSG_BUILD_LOCALITY_PIVOTS",
-         "split": "VSG_BUILD_SPLIT", "bhash": "VSG_BUILD_HASH_FACTOR"}
+         "split": "VSG_BUILD_SPLIT", "bhash": "VSG_BUILD_HASH_FACTOR", "hmin": "VSG_SEARCH_HASH_MIN"}
 
 
 def parse():

@@ -1696,7 +1696,10 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
             const bool reg = env_double("VSG_SEARCH_REG", 1) != 0;
             // register kernel: sweep in profiles/r01_search_hash_reg.jsonl
             const int factor = (int)env_double("VSG_SEARCH_HASH_FACTOR", wide ? (reg ? 8 : 12) : (reg ? 4 : 6));
-            p.hash_size = std::max(hash_size_for(p.ef, factor), wide ? 2048 : 1024);
+            // VSG_SEARCH_HASH_MIN (probes): smallest table (entries, multiple of 64)
+            const int hmin = std::max(64, (int)env_double("VSG_SEARCH_HASH_MIN", wide ? 2048 : 1024)) & ~63;
+            const int raw = std::min(16384, (int)(((long)factor * p.ef + 63) & ~63L));
+            p.hash_size = std::max(raw, hmin);
         }
         // waves per query: 1 = hnsw_search_kernel; 2 / 4 = cooperative kernel
         // (large ef, where one wave is latency-bound on the list).  Same results;

@@ -88,3 +88,50 @@ def test_merge_topk_cpu_padding_and_ties():
     mk, md = merge_topk(gk, gd, 3)
     assert mk.tolist() == [[3, 5, 4]]
     assert md.tolist() == [[1.0, 1.0, 1.5]]
+
+
+def _hybrid_worker(rank, world, S, port, n, dim, nq, k, out_dir):
+    """bench.py's hybrid layout: world / S replica groups of S row shards; each group
+    serves its own query batch, all-gathering inside its subgroup only."""
+    sys.path.insert(0, os.path.join(ROOT, "vector-store-text_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from vsg import datagen as G
+    from vsg.distributed import gather_topk, merge_topk, shard_range
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    groups = [dist.new_group(list(range(g * S, (g + 1) * S))) for g in range(world // S)]
+    grp, srank = rank // S, rank % S
+    pg = groups[grp]
+    x = G.uint8_valued(n, dim, 17)
+    q = G.uint8_valued(nq * (world // S), dim, 18)[grp * nq:(grp + 1) * nq]  # this group's batch
+    lo, hi = shard_range(n, srank, S)
+    keys = np.arange(lo, hi, dtype=np.uint64)
+    ok, od, _ = O.exact_search("l2sq", x[lo:hi], q, k, keys=keys)
+    gk, gd = gather_topk(torch.from_numpy(ok.view(np.int64)), torch.from_numpy(od), pg)
+    assert gk.shape == (S, nq, k)
+    mk, md = merge_topk(gk, gd, k)
+    np.save(os.path.join(out_dir, f"hkeys{rank}.npy"), mk.numpy())
+    np.save(os.path.join(out_dir, f"hdist{rank}.npy"), md.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_hybrid_groups_match_single_index(tmp_path):
+    """4 ranks = 2 groups x 2 row shards (bench.py --multi hybrid): every rank of group g
+    returns the single index's exact top-k of group g's queries."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from vsg import datagen as G
+
+    world, S, n, dim, nq, k = 4, 2, 2001, 16, 30, 10
+    mp.start_processes(_hybrid_worker, args=(world, S, _free_port(), n, dim, nq, k, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    x = G.uint8_valued(n, dim, 17)
+    qa = G.uint8_valued(nq * (world // S), dim, 18)
+    for r in range(world):
+        g = r // S
+        ok, od, _ = O.exact_search("l2sq", x, qa[g * nq:(g + 1) * nq], k)
+        np.testing.assert_array_equal(np.load(tmp_path / f"hkeys{r}.npy").view(np.uint64), ok)
+        np.testing.assert_array_equal(np.load(tmp_path / f"hdist{r}.npy"), od)

@@ -7,17 +7,19 @@ One step = one HNSW search pass of the query batch (10,000 queries, inputs
 resident in HBM) at the smallest ef whose recall@10 against exact ground truth is
 >= 0.95 (ef swept on a 1,000-query subset).
 
-N > 1 (--multi both, default) measures two legs in one run:
-  * shard (`value`, the north-star layout): rank r owns rows [r N/G, (r+1) N/G)
-    of the 1M index, every query is searched on every shard, the per-shard top-k'
-    is all-gathered over RCCL (xGMI) and k-way merged by the HIP merge kernel;
-    (ef, k') re-tuned for merged recall >= 0.95; total work fixed => "scaling":
-    "strong", value = queries / max-over-ranks time.  The build is sharded too
-    (every rank builds N/G rows, no communication).
-  * replica (`replica_mode`, beside it): every rank holds the whole 1M index
-    (3 GB of 288 GB HBM) and serves its own 10,000-query batch per step (weak).
-DESIGN.md §6 explains why replicas maximise QPS when the index fits one GPU and
-shards win the build; the headline follows the north star's layout.
+N > 1 (--multi all, default) measures up to three layouts in one run:
+  * shard: rank r owns rows [r N/G, (r+1) N/G) of the 1M index, every query is
+    searched on every shard, the per-shard top-k' is all-gathered over RCCL (xGMI)
+    and k-way merged by the HIP merge kernel; (ef, k') re-tuned for merged recall
+    >= 0.95; total work fixed => "strong".  The build is sharded too.
+  * replica: every rank holds the whole 1M index (3 GB of 288 GB HBM) and serves
+    its own 10,000-query batch per step (weak).
+  * hybrid (N >= 4, --shards-per-group S=2): N/S groups of S row shards, each
+    group serving its own batch, all-gather inside the group only (weak).
+`value` is the hybrid leg when it ran (N = 4, 8), else the shard leg (N = 2); the
+others are reported beside it.  DESIGN.md §6 explains the trade-off (replicas
+maximise QPS when the index fits one GPU, shards win the build and the recall-ef).
+With --abi-leg 1 rank 0 also times the one-process sharded C ABI (vsg_sharded_*).
 
 Also reported: build vectors/s (GPU batched HNSW build of the whole index, max over
 ranks), the HBM roofline of the search kernel (algorithmic bytes counted by the

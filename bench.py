@@ -534,7 +534,11 @@ def main():
         res[list(res)[-1]].pop("index", None)
         c.barrier()
         if rank == 0:
-            out["sharded_abi"] = abi_leg(c)
+            # a failure here is reported in the line, never loses the measured legs
+            try:
+                out["sharded_abi"] = abi_leg(c)
+            except Exception as e:  # noqa: BLE001
+                out["sharded_abi"] = {"error": f"{type(e).__name__}: {e}"[:400]}
         c.barrier()
     # CPU baseline (rank 0, N=1 only): oracle/ restatement of usearch
     if world == 1 and rank == 0 and not a.no_cpu:

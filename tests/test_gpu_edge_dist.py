@@ -75,3 +75,39 @@ def test_import_and_load_then_add_fill_the_distances(tmp_path, monkeypatch):
             res.append(c.export())
     _same(res[0], res[1])
     _same(res[0], res[2])
+
+
+def test_add_to_imported_graph_without_upper_rows(tmp_path, monkeypatch):
+    """a loaded / imported graph with no level > 0 node has no upper
+    distance table; adding a level-0 vector must fill the level-0 distances only and
+    build the oracle's graph (the 6-node ring case), through import and through load."""
+    dim = 16
+    x = G.uint8_valued(8, dim, 93)
+    for seed in range(1, 200):
+        h = O.HnswOracle(dim, "l2sq", 16, 64, 48, seed=seed)
+        h.add(np.arange(6), x[:6], threads=1)
+        g = h.export()
+        if g["max_level"] != 0:
+            continue
+        h.add([6], x[6:7], threads=1)
+        want = h.export()
+        if want["max_level"] != 0:
+            continue  # the new node would bring upper rows: not the case under test
+        res = []
+        for flag in ("0", "1"):
+            monkeypatch.setenv("VSG_BUILD_EDGE_DIST", flag)
+            a = vsg.Index(dim, "l2sq", "f32", 16, 64, 48, seed=seed)
+            a.import_graph(g)
+            a.add([6], x[6:7])
+            res.append(a.export())
+        p = tmp_path / "ring.vsg"
+        b = vsg.Index(dim, "l2sq", "f32", 16, 64, 48, seed=seed)
+        b.import_graph(g)
+        b.save(p)
+        c = vsg.Index.load(p)
+        c.add([6], x[6:7])
+        res.append(c.export())
+        for r in res:
+            _same(r, want)
+        return
+    pytest.fail("no seed in 1..199 gave a level-0 graph")

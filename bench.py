@@ -91,6 +91,8 @@ def parse():
                          "all = every leg, the hybrid one as value; both = shard (value) + replica")
     ap.add_argument("--shards-per-group", type=int, default=2,
                     help="hybrid leg: GPUs (row shards) per replica group")
+    ap.add_argument("--streams-leg", type=int, default=2,
+                    help="N=1: also time the K steps round-robin over this many streams (0/1: off)")
     ap.add_argument("--abi-leg", type=int, default=1,
                     help="N>1: also time the drop-in's own multi-GPU path -- one vsg_sharded_t over all N "
                          "devices in rank 0's process (include/vsg.h vsg_sharded_*), peer-DMA gather + HIP merge")
@@ -283,7 +285,9 @@ def hnsw_leg(c, mode):
     ev1 = torch.cuda.Event(enable_timing=True)
     # Steps are enqueued back to back (no host round trip between them); the
     # shard leg alternates two streams so one step's all-gather + merge (latency-
-    # bound) runs under the next step's search.  Every step's search,
+    # bound) runs under the next step's search, while the searches
+    # themselves stay one after another (each waits for the previous one's end
+    # event), so the HIP events time one launch each.  Every step's search,
     # gather and merge run inside the timed region; barrier + synchronize on both
     # sides.
     streams = [c.stream, torch.cuda.Stream(device=c.dev)] if sharded else [c.stream]
@@ -293,6 +297,8 @@ def hnsw_leg(c, mode):
     for i in range(a.steps):
         s = streams[i % len(streams)]
         with torch.cuda.stream(s):
+            if i and s is not streams[(i - 1) % len(streams)]:
+                s.wait_event(evs[i - 1][1])
             evs[i][0].record(s)
             keys, dists = index.search_device(q, ks, ef, stream=s)
             evs[i][1].record(s)
@@ -307,6 +313,30 @@ def hnsw_leg(c, mode):
     alg_bytes = (st["search_distances"] * row_bytes + st["search_adjacency"] * 2 * a.M * 4) / a.steps
     kern_ms_avg = kern_ms / a.steps
 
+    # the same K steps spread over --streams-leg streams (beside the headline, never
+    # `value`): a step may start while the previous one's last partial round of
+    # resident waves drains, as concurrent clients of one index would run them
+    # (each search takes its own scratch set, csrc/vsg_index.cpp ws_acquire)
+    conc = None
+    if a.streams_leg > 1 and not sharded and world == 1:
+        ss = [c.stream] + [torch.cuda.Stream(device=c.dev) for _ in range(a.streams_leg - 1)]
+        outs = [(torch.empty((a.queries, ks), dtype=torch.int64, device=c.dev),
+                 torch.empty((a.queries, ks), dtype=torch.float32, device=c.dev)) for _ in ss]
+        for j, sj in enumerate(ss):  # warm-up: one scratch set per stream
+            sj.wait_stream(c.stream)
+            index.search_device(q, ks, ef, out_keys=outs[j][0], out_dist=outs[j][1], stream=sj)
+        c.barrier()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            j = i % len(ss)
+            index.search_device(q, ks, ef, out_keys=outs[j][0], out_dist=outs[j][1], stream=ss[j])
+        c.barrier()
+        el_c = c.max_over_ranks(time.perf_counter() - t0)
+        same = all(torch.equal(o[0], keys) and torch.equal(o[1], dists) for o in outs)
+        conc = {"streams": len(ss), "qps": round(queries_done / el_c, 1), "ms_per_step": round(1000.0 * el_c / a.steps, 3),
+                "results_equal_single_stream": bool(same),
+                "note": "same K steps and ef, round-robin over the streams: a step's search may start while the "
+                        "previous one drains its last partial round of waves (serving with concurrent clients)"}
     # the config's nominal efSearch, timed the same way (reported beside the headline)
     at_cfg = None
     if a.config_ef and a.config_ef != ef:
@@ -383,6 +413,7 @@ def hnsw_leg(c, mode):
         index.set_f16_traversal(False)
         index.set_upper_ef(0)
     return {
+        "concurrent": conc,
         "multi_entry": multi,
         "f16_rerank": rerank,
         "mode": mode, "index": index, "q": q, "x": x, "nloc": nloc, "shards": sworld, "groups": ngrp,
@@ -508,6 +539,7 @@ def main():
         "at_config_ef": head["at_config_ef"],
         "f16_traversal_rerank": head.get("f16_rerank"),
         "multi_entry": head.get("multi_entry"),
+        "concurrent_streams": head.get("concurrent"),
     }
     notes = {"replica": "every rank holds the whole index and serves its own query batch",
              "shard": "every query searched on all N row shards, all-gather + merge (the north star's layout)",

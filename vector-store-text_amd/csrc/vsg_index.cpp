@@ -195,6 +195,7 @@ struct Workspace {
     size_t cap = 0;
     hipEvent_t done = nullptr;
     bool pending = false;
+    hipStream_t last = nullptr;  // stream of the last search that used it
     ~Workspace() {
         if (pending) (void)hipEventSynchronize(done);
         if (base) (void)hipFree(base);
@@ -366,6 +367,7 @@ struct vsg_index {
     std::mutex ctx_mu;
     std::vector<SearchCtx*> ctx_free;  // idle search contexts
     std::vector<Workspace*> ws_free;   // idle device scratch (guarded by ctx_mu)
+    size_t ws_count = 0;               // workspaces in existence (free or in use)
     uint32_t* d_rm = nullptr;          // remove(): slot list (writer side)
     size_t rm_cap = 0;
 
@@ -392,6 +394,7 @@ static void free_dev(vsg_index* h) {
     for (SearchCtx* c : h->ctx_free) delete c;
     h->ctx_free.clear();
     for (Workspace* w : h->ws_free) delete w;
+    h->ws_count -= std::min(h->ws_count, h->ws_free.size());
     h->ws_free.clear();
     hipFree(h->d_rm);
     hipFree(h->d_vecs);
@@ -1396,28 +1399,48 @@ int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_r
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Up to WS_MAX searches on different streams run concurrently, each in its own
+// scratch set: a workspace last used on another stream whose search is still
+// running is reused only once WS_MAX exist (then the new search waits for it).
+// Until round 4 every call took the one released workspace and waited for its
+// previous search, so searches issued on two streams never overlapped.
+constexpr size_t WS_MAX = 4;
+
 static int ws_acquire(vsg_index* h, size_t bytes, hipStream_t s, Workspace** out) {
     Workspace* w = nullptr;
     {
         std::lock_guard<std::mutex> lk(h->ctx_mu);
-        // smallest idle workspace that fits, else the largest (grown below)
+        // 1. the smallest free workspace that fits and needs no cross-stream wait
+        // 2. a new one while fewer than WS_MAX exist
+        // 3. the smallest that fits (waiting for it), else the largest (grown below)
         const size_t none = h->ws_free.size();
-        size_t fit = none, big = none;
+        size_t ready = none, fit = none, big = none;
         for (size_t i = 0; i < none; ++i) {
-            const size_t c = h->ws_free[i]->cap;
-            if (c >= bytes && (fit == none || c < h->ws_free[fit]->cap)) fit = i;
-            if (big == none || c > h->ws_free[big]->cap) big = i;
+            Workspace* c = h->ws_free[i];
+            if (c->pending && c->last != s && hipEventQuery(c->done) == hipSuccess) c->pending = false;
+            const bool nowait = !c->pending || c->last == s;
+            if (c->cap >= bytes && nowait && (ready == none || c->cap < h->ws_free[ready]->cap)) ready = i;
+            if (c->cap >= bytes && (fit == none || c->cap < h->ws_free[fit]->cap)) fit = i;
+            if (big == none || c->cap > h->ws_free[big]->cap) big = i;
         }
-        const size_t best = fit != none ? fit : big;
-        if (best < h->ws_free.size()) {
+        size_t best = ready;
+        if (best == none && h->ws_count >= WS_MAX) best = fit != none ? fit : big;
+        if (best < none) {
             w = h->ws_free[best];
             h->ws_free.erase(h->ws_free.begin() + (long)best);
+        } else {
+            ++h->ws_count;  // reserved before the allocation below
         }
     }
+    auto drop = [&](Workspace* d) {
+        delete d;
+        std::lock_guard<std::mutex> lk(h->ctx_mu);
+        --h->ws_count;
+    };
     if (!w) {
         w = new Workspace;
         if (hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess) {
-            delete w;
+            drop(w);
             return fail(VSG_EDEVICE, "hipEventCreate failed");
         }
     }
@@ -1429,11 +1452,11 @@ static int ws_acquire(vsg_index* h, size_t bytes, hipStream_t s, Workspace** out
         const size_t want = std::max(bytes, w->cap * 2);
         w->cap = 0;
         if (hipMalloc((void**)&w->base, want) != hipSuccess) {
-            delete w;
+            drop(w);
             return fail(VSG_ENOMEM, "search workspace");
         }
         w->cap = want;
-    } else if (w->pending) {
+    } else if (w->pending && w->last != s) {
         const hipError_t e = hipStreamWaitEvent(s, w->done, 0);
         if (e != hipSuccess) {
             std::lock_guard<std::mutex> lk(h->ctx_mu);
@@ -1447,6 +1470,7 @@ static int ws_acquire(vsg_index* h, size_t bytes, hipStream_t s, Workspace** out
 
 static void ws_release(vsg_index* h, Workspace* w, hipStream_t s) {
     w->pending = hipEventRecord(w->done, s) == hipSuccess;
+    w->last = s;
     if (!w->pending) (void)hipStreamSynchronize(s);
     std::lock_guard<std::mutex> lk(h->ctx_mu);
     h->ws_free.push_back(w);

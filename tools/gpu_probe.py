@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--sort-base", action="store_true",
                     help="build: rows inserted in synthetic-cluster order (slot ids spatial; probe of "
                          "VSG_BUILD_LOCALITY=2)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="search: also time the steps round-robin over this many streams (wall clock; "
+                         "sustained algorithmic bytes / wall)")
     ap.add_argument("--seeds", default="0", help="index seeds (offsets from the default; search mode: the first)")
     ap.add_argument("--phases", action="store_true",
                     help="build mode, with VSG_LIB_PATH=lib_prof/libvsg.so (make prof): insert-wave "
@@ -173,7 +176,21 @@ def main():
             nq = max(1, s["search_queries"])
             alg = (s["search_distances"] * row_bytes + s["search_adjacency"] * 2 * a.M * 4) / a.steps
             gbs = alg / (ms_k * 1e-3) / 1e9
-            print(json.dumps(dict(head, ef=ef, set=st, kernel_ms=round(ms_k, 3), qps=round(a.queries / ms_k * 1e3, 1),
+            multi = {}
+            if a.streams > 1:
+                ss = [torch.cuda.Stream() for _ in range(a.streams)]
+                for sj in ss:  # one scratch set per stream
+                    idx.search_device(q, a.k, ef, stream=sj)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i in range(a.steps):
+                    idx.search_device(q, a.k, ef, stream=ss[i % a.streams])
+                torch.cuda.synchronize()
+                wall = (time.perf_counter() - t0) / a.steps
+                multi = {"streams": a.streams, "streams_ms_per_step": round(wall * 1e3, 3),
+                         "streams_qps": round(a.queries / wall, 1),
+                         "streams_sustained_frac": round(alg / wall / 1e9 / 8000.0, 4)}
+            print(json.dumps(dict(head, **multi, ef=ef, set=st, kernel_ms=round(ms_k, 3), qps=round(a.queries / ms_k * 1e3, 1),
                                   dist_per_query=round(s["search_distances"] / nq, 1),
                                   adj_per_query=round(s["search_adjacency"] / nq, 1),
                                   alg_bytes_per_launch=int(alg), achieved_gbs=round(gbs, 1),

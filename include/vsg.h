@@ -314,9 +314,10 @@ typedef struct {
     uint32_t max_wait_us;       /* optional coalescing window; 0 => natural batching */
     uint32_t compact_percent;   /* vsg_index_compact once tombstones >= this % of stored
                                    rows; 0 => 50, >= 100 => never */
-    uint32_t concurrent_reads;  /* 1: anns run on a second worker beside the writes and see a
-                                   prefix of them (the reference's fire-and-forget adds,
-                                   usearch.rs:200-221); 0: submission order (default) */
+    uint32_t concurrent_reads;  /* n >= 1: anns run on n read workers beside the writes and see
+                                   a prefix of them (the reference's fire-and-forget adds,
+                                   usearch.rs:200-221); n >= 2 keeps n search batches in
+                                   flight (capped at 8); 0: submission order (default) */
     uint64_t compact_min_dead;  /* ... and at least this many; 0 => 4096 */
 } vsg_actor_options_t;
 

@@ -211,8 +211,9 @@ pub(crate) fn new(
         // reserve(RESERVE_INCREMENT) up front and the growth rule of usearch.rs:200-212
         reserve_increment: 1_000_000,
         reserve_threshold: 1_000_000 / 3,
-        // anns beside writes, as the reference's fire-and-forget adds allow
-        concurrent_reads: 1,
+        // anns beside writes, as the reference's fire-and-forget adds allow, on two
+        // read workers: two search batches in flight overlap one's GPU tail with the next
+        concurrent_reads: 2,
         ..Default::default()
     };
     let keys: Keys = Arc::new(RwLock::new(KeyMap { map: BiMap::new(), next: 0 }));

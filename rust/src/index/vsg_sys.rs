@@ -84,7 +84,7 @@ pub struct vsg_actor_options_t {
     pub max_batch: u32,         // 0 => 65536 messages per drain
     pub max_wait_us: u32,       // 0 => natural batching
     pub compact_percent: u32,   // 0 => 50
-    pub concurrent_reads: u32,  // 1 => anns beside writes (the reference's fire-and-forget adds)
+    pub concurrent_reads: u32,  // n >= 1 => anns on n read workers beside writes (the reference's fire-and-forget adds)
     pub compact_min_dead: u64,  // 0 => 4096
 }
 

@@ -446,8 +446,75 @@ static void test_concurrent_reads_beside_writes() {
     }
 }
 
+// 7) concurrent_reads = 2: two Anns from two clients are searched at the same time
+//    (a backend whose search takes 100 ms answers both in ~100 ms, not ~200 ms),
+//    with the results one reader gives.
+struct SlowSearch final : vsg::ActorBackend {
+    std::atomic<int> in_flight{0}, max_in_flight{0};
+    size_t dimensions() const override { return 1; }
+    size_t size() const override { return 3; }
+    size_t capacity() const override { return 1000; }
+    size_t expansion_search() const override { return 16; }
+    bool contains(uint64_t) const override { return false; }
+    int reserve(size_t) override { return 0; }
+    int add(const uint64_t*, const float*, size_t) override { return 0; }
+    int remove(const uint64_t*, size_t, size_t* r) override {
+        if (r) *r = 0;
+        return 0;
+    }
+    int search(const float* q, size_t nq, size_t k, size_t, uint64_t* keys, float* dist, size_t* counts) override {
+        const int now = ++in_flight;
+        int m = max_in_flight.load();
+        while (now > m && !max_in_flight.compare_exchange_weak(m, now)) {
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+        for (size_t i = 0; i < nq; ++i) {
+            for (size_t j = 0; j < k; ++j) {
+                keys[i * k + j] = (uint64_t)(q[i] * 10) + j;
+                dist[i * k + j] = (float)j;
+            }
+            counts[i] = k;
+        }
+        --in_flight;
+        return 0;
+    }
+};
+
+static void test_read_workers_overlap() {
+    for (uint32_t readers : {2u, 1u}) {
+        auto* m = new SlowSearch;
+        SlowSearch* mp = m;
+        vsg::ActorConfig cfg;
+        cfg.concurrent_reads = readers;
+        vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), cfg);
+        CHECK(a.init() == 0);
+        uint64_t ka[2], kb[2];
+        float da[2], db[2];
+        size_t ca = 0, cb = 0;
+        int ra = -1, rb = -1;
+        const float qa = 1.f, qb = 2.f;
+        const auto t0 = std::chrono::steady_clock::now();
+        std::thread ta([&] { ra = a.ann(&qa, 1, 2, ka, da, &ca); });
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        std::thread tb([&] { rb = a.ann(&qb, 1, 2, kb, db, &cb); });
+        ta.join();
+        tb.join();
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        CHECK(ra == 0 && rb == 0 && ca == 2 && cb == 2);
+        CHECK(ka[0] == 10 && ka[1] == 11 && kb[0] == 20 && kb[1] == 21);
+        if (readers == 2) {
+            CHECK(mp->max_in_flight.load() == 2);
+            CHECK(ms < 180.0);
+        } else {
+            CHECK(mp->max_in_flight.load() == 1);
+            CHECK(ms > 190.0);
+        }
+    }
+}
+
 int main() {
     test_concurrent_reads_beside_writes();
+    test_read_workers_overlap();
     test_fifo_semantics();
     test_concurrent_anns();
     test_ef_groups_and_errors();

@@ -6,7 +6,7 @@
 //     vsg_index_new -> vsg_index_reserve(1M) -> vsg_index_add -> replace
 //     (vsg_index_remove + vsg_index_add of the same key) -> vsg_index_search ->
 //     vsg_index_size -> vsg_index_free;
-//  2. the actor path gpu.rs uses (vsg_actor_*, concurrent_reads = 1): the reference's own
+//  2. the actor path gpu.rs uses (vsg_actor_*, concurrent_reads = 2): the reference's own
 //     unit KAT (usearch.rs:322-425, D = 3, keys 1/2/3, replace, remove, count) with its
 //     polling (anns may run before earlier writes land, as the reference's fire-and-forget
 //     adds allow; it polls for 10 s, usearch.rs:352-358).  Adds go through
@@ -98,7 +98,7 @@ static void actor_kat(bool sharded) {
     o.index.metric = VSG_METRIC_L2SQ;
     o.reserve_increment = 1000000;  // RESERVE_INCREMENT, usearch.rs:62
     o.reserve_threshold = 1000000 / 3;
-    o.concurrent_reads = 1;  // as rust/src/index/gpu.rs
+    o.concurrent_reads = 2;  // as rust/src/index/gpu.rs
     vsg_actor_t* a = nullptr;
     const int32_t devs[2] = {0, 0};
     if (sharded) {

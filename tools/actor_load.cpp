@@ -7,6 +7,7 @@
 //
 // build: make -C tools actor_load   (links ../vector-store-text_amd/lib/libvsg.so)
 // usage: actor_load rows dim metric(0 l2sq,1 ip,2 cos) clients queries_per_client k ef [max_wait_us]
+//        [read_workers: 0 = anns on the one FIFO worker; n = concurrent_reads n]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,7 +33,7 @@ using clk = std::chrono::steady_clock;
 
 int main(int argc, char** argv) {
     if (argc < 8) {
-        std::fprintf(stderr, "usage: %s rows dim metric clients qpc k ef [max_wait_us]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s rows dim metric clients qpc k ef [max_wait_us] [read_workers]\n", argv[0]);
         return 2;
     }
     const size_t rows = std::strtoull(argv[1], nullptr, 10), dim = std::strtoull(argv[2], nullptr, 10);
@@ -40,6 +41,7 @@ int main(int argc, char** argv) {
     const int clients = std::atoi(argv[4]), qpc = std::atoi(argv[5]);
     const size_t k = std::strtoull(argv[6], nullptr, 10), ef = std::strtoull(argv[7], nullptr, 10);
     const unsigned wait_us = argc > 8 ? (unsigned)std::atoi(argv[8]) : 0;
+    const unsigned readers = argc > 9 ? (unsigned)std::atoi(argv[9]) : 0;
     const uint64_t cfg = 2, base_seed = 0x5EED0000 + cfg, q_seed = 0x5EED1000 + cfg, m_seed = 0x5EED2000 + cfg;
 
     vsg_actor_options_t o{};
@@ -50,6 +52,7 @@ int main(int argc, char** argv) {
     o.index.expansion_search = (uint32_t)ef;
     o.index.seed = 1;
     o.max_wait_us = wait_us;
+    o.concurrent_reads = readers;
     vsg_actor_t* a = nullptr;
     TRY(vsg_actor_new(&o, &a));
     vsg_index_t* h = vsg_actor_index(a);
@@ -148,10 +151,10 @@ int main(int argc, char** argv) {
     const uint64_t calls = c1.search_calls - c0.search_calls;
     std::printf(
         "{\"rows\": %zu, \"dim\": %zu, \"clients\": %d, \"queries\": %zu, \"k\": %zu, \"ef\": %zu, "
-        "\"max_wait_us\": %u, \"actor_qps\": %.1f, \"batched_qps\": %.1f, \"lat_us_p50\": %.1f, "
+        "\"max_wait_us\": %u, \"read_workers\": %u, \"actor_qps\": %.1f, \"batched_qps\": %.1f, \"lat_us_p50\": %.1f, "
         "\"lat_us_p99\": %.1f, \"search_calls\": %llu, \"mean_batch\": %.1f, \"max_batch\": %llu, "
         "\"mismatch_vs_batched\": %d, \"errors\": %d}\n",
-        rows, dim, clients, nq, k, ef, wait_us, nq / served_s, nq / batched_s, lat[nq / 2], lat[nq * 99 / 100],
+        rows, dim, clients, nq, k, ef, wait_us, readers, nq / served_s, nq / batched_s, lat[nq / 2], lat[nq * 99 / 100],
         (unsigned long long)calls, calls ? (double)nq / calls : 0.0, (unsigned long long)c1.max_search_batch,
         mismatch.load(), errors.load());
     vsg_actor_free(a);

@@ -14,11 +14,12 @@
 //   * count = live size                                            :308-311
 // Ordering, default: stronger than the reference's (which spawns every message
 // as its own task): messages are applied in submission order, so an Ann sees
-// every write submitted before it.  With concurrent_reads, Anns go to a second
-// worker that searches while the writer builds (the reference's behaviour:
+// every write submitted before it.  With concurrent_reads = n, Anns go to n read
+// workers that search while the writer builds (the reference's behaviour:
 // add is fire-and-forget on rayon, search runs beside it under the shared lock,
 // usearch.rs:200-221, :274-277): an Ann then sees a prefix of the writes, and a
-// burst of inserts no longer delays queries by the whole batched build.
+// burst of inserts no longer delays queries by the whole batched build.  n >= 2
+// keeps n search batches in flight, so one batch's GPU tail overlaps the next.
 // Batching never changes a result: an Ann run is split by effective ef =
 // max(ef, k) and a query's top-k is the prefix of its group's top-kmax (the
 // search returns the first k live entries of its list).
@@ -72,9 +73,12 @@ struct ActorConfig {
     // as a tombstone (usearch.rs:214-221), so an upsert stream needs this.
     uint32_t compact_percent = 50;
     size_t compact_min_dead = 4096;
-    // Anns on their own worker, beside the writes (needs a backend whose search
-    // may run concurrently with add/remove, as vsg_index's does)
-    bool concurrent_reads = false;
+    // Anns on their own workers, beside the writes (needs a backend whose search
+    // may run concurrently with add/remove, as vsg_index's does): 0 = submission
+    // order on the one worker; n >= 1 = n read workers, so up to n search batches
+    // are in flight at once (the GPU overlaps one batch's tail with the next,
+    // DESIGN.md §3.2); at most 8
+    uint32_t concurrent_reads = 0;
 };
 
 struct ActorCounters {
@@ -128,8 +132,9 @@ class Actor {
 
     Actor(std::unique_ptr<ActorBackend> be, const ActorConfig& cfg) : be_(std::move(be)), cfg_(cfg) {
         if (cfg_.max_batch == 0) cfg_.max_batch = 1;
+        if (cfg_.concurrent_reads > 8) cfg_.concurrent_reads = 8;
         worker_ = std::thread([this] { run(q_, qcv_); });
-        if (cfg_.concurrent_reads) reader_ = std::thread([this] { run(rq_, rcv_); });
+        for (uint32_t i = 0; i < cfg_.concurrent_reads; ++i) readers_.emplace_back([this] { run(rq_, rcv_); });
     }
 
     ~Actor() {
@@ -140,7 +145,7 @@ class Actor {
         qcv_.notify_all();
         rcv_.notify_all();
         worker_.join();
-        if (reader_.joinable()) reader_.join();
+        for (std::thread& t : readers_) t.join();
     }
 
     // initial reservation, usearch.rs:99
@@ -220,7 +225,7 @@ class Actor {
 
   private:
     void push(Msg&& m) {
-        const bool read = cfg_.concurrent_reads && m.kind == ANN;
+        const bool read = cfg_.concurrent_reads > 0 && m.kind == ANN;
         {
             std::lock_guard<std::mutex> lk(qm_);
             (read ? rq_ : q_).push_back(std::move(m));
@@ -435,7 +440,8 @@ class Actor {
     bool stop_ = false;
     mutable std::mutex cm_;
     ActorCounters ctr_;
-    std::thread worker_, reader_;
+    std::thread worker_;
+    std::vector<std::thread> readers_;
 };
 
 }  // namespace vsg

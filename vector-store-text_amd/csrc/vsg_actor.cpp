@@ -84,7 +84,7 @@ vsg::ActorConfig actor_config(const vsg_actor_options_t* o) {
     cfg.max_wait_us = o->max_wait_us;
     if (o->compact_percent) cfg.compact_percent = o->compact_percent;
     if (o->compact_min_dead) cfg.compact_min_dead = o->compact_min_dead;
-    cfg.concurrent_reads = o->concurrent_reads != 0;
+    cfg.concurrent_reads = o->concurrent_reads;  // 0, 1, or n read workers (capped at 8)
     return cfg;
 }
 

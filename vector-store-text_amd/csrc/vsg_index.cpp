@@ -330,6 +330,18 @@ struct vsg_index {
     uint32_t* d_pv[2] = {nullptr, nullptr};
     size_t pairs_cap = 0;
     void* d_sort_tmp = nullptr;
+    // build scratch outgrown during an add: freed once the add's stream drained
+    // (hipFree synchronises the device, which would stall the host's planning
+    // until the locality cells enqueued just before had finished)
+    std::vector<void*> defer_free;
+    // pinned host staging of an add's plan (insertion order, levels, pair and
+    // list offsets): pageable hipMemcpyAsync blocks the host until the stream
+    // reaches the copy, i.e. until the locality cells enqueued before it ran
+    uint8_t* h_plan = nullptr;
+    size_t h_plan_cap = 0;
+    // pinned staging of stage_slots' uploads (keys | upper-row offsets), same reason
+    uint8_t* h_stg = nullptr;
+    size_t h_stg_cap = 0;
     size_t sort_tmp_bytes = 0;
     float* d_stage = nullptr;
     size_t stage_cap = 0;  // rows
@@ -388,7 +400,16 @@ struct vsg_index {
     }
 };
 
+static void flush_deferred(vsg_index* h);
+
 static void free_dev(vsg_index* h) {
+    flush_deferred(h);  // hipFree waits for the device
+    if (h->h_plan) (void)hipHostFree(h->h_plan);
+    h->h_plan = nullptr;
+    h->h_plan_cap = 0;
+    if (h->h_stg) (void)hipHostFree(h->h_stg);
+    h->h_stg = nullptr;
+    h->h_stg_cap = 0;
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     h->ev_pool.clear();
     for (SearchCtx* c : h->ctx_free) delete c;
@@ -498,18 +519,24 @@ static int ensure_buf(X** p, size_t& cap, size_t need) {
     return VSG_OK;
 }
 
+// release a build scratch buffer after the add's device work (flush_deferred)
+template <typename X> static void dfree(vsg_index* h, X*& p) {
+    if (p) h->defer_free.push_back((void*)p);
+    p = nullptr;
+}
+static void flush_deferred(vsg_index* h) {
+    for (void* p : h->defer_free) (void)hipFree(p);
+    h->defer_free.clear();
+}
+
 // per-add node buffers (levels, pair offsets) and per-batch pair buffers
 static int ensure_nodes(vsg_index* h, size_t n) {
     if (n <= h->bnodes_cap) return VSG_OK;
     const size_t want = std::max(n, h->bnodes_cap * 2);
-    hipFree(h->d_blevels);
-    hipFree(h->d_pair_off);
-    hipFree(h->d_bnodes);
-    hipFree(h->d_list_off);
-    h->d_blevels = nullptr;
-    h->d_pair_off = nullptr;
-    h->d_bnodes = nullptr;
-    h->d_list_off = nullptr;
+    dfree(h, h->d_blevels);
+    dfree(h, h->d_pair_off);
+    dfree(h, h->d_bnodes);
+    dfree(h, h->d_list_off);
     h->bnodes_cap = 0;
     HIP_TRY(dev_alloc(&h->d_blevels, want));
     HIP_TRY(dev_alloc(&h->d_pair_off, want));
@@ -522,12 +549,9 @@ static int ensure_nodes(vsg_index* h, size_t n) {
 static int ensure_lists(vsg_index* h, size_t lists) {
     if (lists <= h->lst_cap) return VSG_OK;
     const size_t want = std::max(lists, h->lst_cap * 2);
-    hipFree(h->d_lst_d);
-    hipFree(h->d_lst_i);
-    hipFree(h->d_lst_n);
-    h->d_lst_d = nullptr;
-    h->d_lst_i = nullptr;
-    h->d_lst_n = nullptr;
+    dfree(h, h->d_lst_d);
+    dfree(h, h->d_lst_i);
+    dfree(h, h->d_lst_n);
     h->lst_cap = 0;
     HIP_TRY(dev_alloc(&h->d_lst_d, want * (size_t)h->efc));
     HIP_TRY(dev_alloc(&h->d_lst_i, want * (size_t)h->efc));
@@ -564,25 +588,21 @@ static int ensure_locality(vsg_index* h, size_t n, size_t max_b, size_t part_ent
     const size_t rf = loc_row_floats(h);
     if (!h->d_piv) HIP_TRY(dev_alloc(&h->d_piv, LOC_PIVOTS * (rf * 4 + 4 + 1 + 4 + 8) + 256));
     if (h->st == ST_F16 && chunk > h->cf32_cap) {
-        hipFree(h->d_cf32);
-        h->d_cf32 = nullptr;
+        dfree(h, h->d_cf32);
         h->cf32_cap = 0;
         HIP_TRY(dev_alloc(&h->d_cf32, chunk * rf));
         h->cf32_cap = chunk;
     }
     if (n > h->cell_cap) {
         const size_t want = std::max(n, h->cell_cap * 2);
-        hipFree(h->d_cell);
-        h->d_cell = nullptr;
+        dfree(h, h->d_cell);
         h->cell_cap = 0;
         HIP_TRY(dev_alloc(&h->d_cell, want));
         h->cell_cap = want;
     }
     if (part_entries > h->cpart_cap) {
-        hipFree(h->d_cpart_d);
-        hipFree(h->d_cpart_i);
-        h->d_cpart_d = nullptr;
-        h->d_cpart_i = nullptr;
+        dfree(h, h->d_cpart_d);
+        dfree(h, h->d_cpart_i);
         h->cpart_cap = 0;
         HIP_TRY(dev_alloc(&h->d_cpart_d, part_entries));
         HIP_TRY(dev_alloc(&h->d_cpart_i, part_entries));
@@ -590,10 +610,8 @@ static int ensure_locality(vsg_index* h, size_t n, size_t max_b, size_t part_ent
     }
     if (max_b > h->border_cap) {
         for (int i = 0; i < 2; ++i) {
-            hipFree(h->d_okey[i]);
-            hipFree(h->d_oidx[i]);
-            h->d_okey[i] = nullptr;
-            h->d_oidx[i] = nullptr;
+            dfree(h, h->d_okey[i]);
+            dfree(h, h->d_oidx[i]);
         }
         h->border_cap = 0;
         for (int i = 0; i < 2; ++i) {
@@ -723,10 +741,8 @@ static int ensure_pairs(vsg_index* h, size_t n) {
     if (n <= h->pairs_cap) return VSG_OK;
     const size_t want = std::max(n, h->pairs_cap * 2);
     for (int i = 0; i < 2; ++i) {
-        hipFree(h->d_pk[i]);
-        hipFree(h->d_pv[i]);
-        h->d_pk[i] = nullptr;
-        h->d_pv[i] = nullptr;
+        dfree(h, h->d_pk[i]);
+        dfree(h, h->d_pv[i]);
     }
     h->pairs_cap = 0;
     for (int i = 0; i < 2; ++i) {
@@ -768,17 +784,52 @@ static int map_keys(vsg_index* h, const uint64_t* keys, size_t n, uint32_t s0) {
 // offsets (the upper table is sized for the whole call here, so the build never
 // reallocates it), keys, flags and upper_off uploaded; `slots` grows.  No link
 // to the new rows exists yet, so searches cannot reach them.
-static int stage_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* keys) {
-    hipStream_t st = h->stream;
-    // levels and upper rows
-    std::vector<uint32_t> upper_off(n);
-    size_t need_upper = h->upper_used;
+// grow a pinned host staging buffer (its previous contents are not kept)
+static int ensure_pinned(uint8_t** p, size_t& cap, size_t need) {
+    if (need <= cap) return VSG_OK;
+    const size_t want = std::max(need, cap * 2);
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    cap = 0;
+    HIP_TRY(hipHostMalloc((void**)p, want, hipHostMallocDefault));
+    cap = want;
+    return VSG_OK;
+}
+
+// Levels of slots [s0, s0 + n) (a pure function of seed and slot) and the upper
+// table sized for them; upper_used is left to stage_slots.  add_common runs it
+// before any device work of the call: the table's growth synchronises the device.
+static int presize_slots(vsg_index* h, uint32_t s0, size_t n) {
     int8_t* lv = h->h_levels.data() + s0;
     const uint32_t M = (uint32_t)h->M;
     const uint64_t seed = h->opt.seed;
     host_parallel(n, [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) lv[i] = (int8_t)sample_level(seed, s0 + i, M);
     });
+    size_t need_upper = h->upper_used;
+    for (size_t i = 0; i < n; ++i) need_upper += (size_t)lv[i];
+    return ensure_upper(h, need_upper);
+}
+
+// sampled: presize_slots already wrote the levels
+static int stage_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* keys, bool sampled = false) {
+    hipStream_t st = h->stream;
+    // keys | upper-row offsets, uploaded from pinned memory: the copies queue
+    // behind the locality cells without blocking the host
+    int rc0 = ensure_pinned(&h->h_stg, h->h_stg_cap, n * 12 + 64);
+    if (rc0) return rc0;
+    uint64_t* kst = reinterpret_cast<uint64_t*>(h->h_stg);
+    uint32_t* upper_off = reinterpret_cast<uint32_t*>(kst + n);
+    std::memcpy(kst, keys, n * 8);
+    // levels and upper rows
+    size_t need_upper = h->upper_used;
+    int8_t* lv = h->h_levels.data() + s0;
+    const uint32_t M = (uint32_t)h->M;
+    const uint64_t seed = h->opt.seed;
+    if (!sampled)
+        host_parallel(n, [&](size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; ++i) lv[i] = (int8_t)sample_level(seed, s0 + i, M);
+        });
     for (size_t i = 0; i < n; ++i) {
         const int L = lv[i];
         upper_off[i] = L > 0 ? (uint32_t)need_upper : 0xFFFFFFFFu;
@@ -787,8 +838,8 @@ static int stage_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* keys
     int rc = ensure_upper(h, need_upper);
     if (rc) return rc;
     h->upper_used = need_upper;
-    HIP_TRY(hipMemcpyAsync(h->d_upper_off + s0, upper_off.data(), n * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(h->d_keys + s0, keys, n * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_upper_off + s0, upper_off, n * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_keys + s0, kst, n * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(h->d_flags + s0, 0, n, st));
     h->slots += n;
     return VSG_OK;
@@ -798,7 +849,15 @@ static int stage_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* keys
 // [s0, s0 + n) whose rows are already in d_vecs.  Writes adjacency rows and the
 // builder's entry point (entry / max_level); searches keep using the published
 // snapshot until publish().
-static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
+// Launch order by locality cell (see ensure_locality) for calls of >= 2 lmin rows
+static size_t locality_min() { return (size_t)env_double("VSG_BUILD_LOCALITY_MIN", 4096); }
+static bool locality_on(const vsg_index* h, size_t n) {
+    return !(h->opt.flags & VSG_FLAG_EXACT_ONLY) && env_double("VSG_BUILD_LOCALITY", 1) != 0 &&
+           loc_row_floats(h) % 32 == 0 && n >= 2 * locality_min();
+}
+
+// cells_done: add_common already enqueued compute_cells for these slots
+static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = false) {
     hipStream_t st = h->stream;
     int rc;
     if (h->opt.flags & VSG_FLAG_EXACT_ONLY) {  // vectors only: no graph
@@ -831,18 +890,22 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     // Insertion order = a seeded pseudo-random permutation of the call's slots:
     // nodes of one batch cannot link to each other, so a batch must not be
     // spatially coherent (a cluster-sorted input otherwise wrecks the graph).
-    std::vector<uint32_t> order(n);
-    std::vector<int8_t> blev(n);
+    // order | pair_off | list_off (n x u32 each) | blev (n x i8), in pinned memory
+    if ((rc = ensure_pinned(&h->h_plan, h->h_plan_cap, n * 13 + 64))) return rc;
+    uint32_t* order = reinterpret_cast<uint32_t*>(h->h_plan);
+    uint32_t* pair_off = order + n;
+    uint32_t* list_off = pair_off + n;
+    int8_t* blev = reinterpret_cast<int8_t*>(list_off + n);
     // VSG_BUILD_PERMUTE: 0 slot order (sequential-build identity tests), 2 serial
     // Fisher-Yates (round 1's order; probes)
     const int pmode = (int)env_double("VSG_BUILD_PERMUTE", 1);
     // Launch order of a batch's nodes: grouped by locality cell for batches of
     // >= lmin nodes (VSG_BUILD_LOCALITY=0: the permutation's order).  The cells
-    // are computed on the device while the host plans.
-    const size_t lmin = (size_t)env_double("VSG_BUILD_LOCALITY_MIN", 4096);
-    const bool locality = env_double("VSG_BUILD_LOCALITY", 1) != 0 && loc_row_floats(h) % 32 == 0 && n >= 2 * lmin;
+    // are computed on the device while the host maps keys (add_common) and plans.
+    const size_t lmin = locality_min();
+    const bool locality = locality_on(h, n);
     std::vector<uint32_t> piv_idx;
-    if (locality && (rc = compute_cells(h, s0, n, piv_idx, st))) return rc;
+    if (locality && !cells_done && (rc = compute_cells(h, s0, n, piv_idx, st))) return rc;
     pc.mark("b:cells_enqueue");
     const uint64_t pkey = host_splitmix64(h->opt.seed ^ 0x5045524D55544Eull ^ (uint64_t)s0);
     const SlotPerm perm(n, pkey);
@@ -884,12 +947,10 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 65536);
     // at least 8 batches per call, so the call's own nodes find each other
     const size_t bcall = std::max<size_t>(1, n / std::max<size_t>(1, (size_t)env_double("VSG_BUILD_MIN_BATCHES", 8)));
-    std::vector<uint32_t> pair_off(n);
     // split insert (launch_insert_split): the efC beam at its own occupancy, then
     // the selection; lists of (node, level) in HBM between the two (VSG_BUILD_SPLIT=0:
     // the fused kernel; efC > 192 always fused)
     const bool split = env_double("VSG_BUILD_SPLIT", 1) != 0 && h->efc <= 192;
-    std::vector<uint32_t> list_off(split ? n : 0);
     size_t max_lists = 0;
     std::vector<Batch> plan;
     size_t max_pairs = 0;
@@ -954,8 +1015,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         size_t tmp = 0;
         HIP_TRY(sort_pairs(nullptr, tmp, h->d_pk[0], h->d_pk[1], h->d_pv[0], h->d_pv[1], max_pairs, st));
         if (tmp > h->sort_tmp_bytes) {
-            hipFree(h->d_sort_tmp);
-            h->d_sort_tmp = nullptr;
+            dfree(h, h->d_sort_tmp);
             h->sort_tmp_bytes = 0;
             HIP_TRY(hipMalloc(&h->d_sort_tmp, tmp * 2));
             h->sort_tmp_bytes = tmp * 2;
@@ -966,10 +1026,10 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
         HIP_TRY(hipEventCreate(&x));
         h->ev_pool.push_back(x);
     }
-    HIP_TRY(hipMemcpyAsync(h->d_bnodes, order.data(), n * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(h->d_blevels, blev.data(), n, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(h->d_pair_off, pair_off.data(), n * 4, hipMemcpyHostToDevice, st));
-    if (split) HIP_TRY(hipMemcpyAsync(h->d_list_off, list_off.data(), n * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_bnodes, order, n * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_blevels, blev, n, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_pair_off, pair_off, n * 4, hipMemcpyHostToDevice, st));
+    if (split) HIP_TRY(hipMemcpyAsync(h->d_list_off, list_off, n * 4, hipMemcpyHostToDevice, st));
     pc.mark("b:buffers+uploads");
 
     // pairs per reverse-kernel wave: with batches of up to 64k nodes, 64 pairs a
@@ -1041,6 +1101,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n) {
     pc.mark("b:enqueue_batches");
     if (!plan.empty()) {
         HIP_TRY(hipStreamSynchronize(st));
+        flush_deferred(h);
         pc.mark("b:device_drain");
         // VSG_DEBUG_TIMING=2: one line per batch (probes)
         const bool per_batch = env_double("VSG_DEBUG_TIMING", 0) >= 2;
@@ -1312,18 +1373,35 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
             if ((rc = reserve_locked(h, std::min<size_t>(want, MAX_SLOTS)))) return rc;
         }
         s0 = (uint32_t)h->slots;
+        if ((rc = presize_slots(h, s0, n))) return rc;
         pc.mark("lock+reserve");
+    }
+    // Rows first, then the locality cells: slots [s0, s0 + n) lie beyond `slots`,
+    // so no search reads them, and a rejected call (reserved or duplicate key)
+    // leaves them as unused capacity.  The device computes the cells while the
+    // host maps the keys (writers are serialised by wmu, so s0 stays valid).
+    // pinned staging first: hipHostMalloc waits for the device, so it must not
+    // come after the cells (stage_slots / build_slots only find it sized)
+    if ((rc = ensure_pinned(&h->h_stg, h->h_stg_cap, n * 12 + 64)) ||
+        (rc = ensure_pinned(&h->h_plan, h->h_plan_cap, n * 13 + 64)))
+        return rc;
+    if ((rc = put_rows(h, vecs, n, device_src, user_stream, s0))) return rc;
+    pc.mark("put_rows");
+    std::vector<uint32_t> piv_idx;  // compute_cells' upload buffer: outlives the add
+    const bool cells = locality_on(h, n);
+    if (cells && (rc = compute_cells(h, s0, n, piv_idx, h->stream))) return rc;
+    pc.mark("cells_enqueue");
+    {
+        std::unique_lock<std::shared_mutex> lk(h->mu);
         if ((rc = map_keys(h, keys, n, s0))) return rc;
         pc.mark("map_keys");
-        if ((rc = stage_slots(h, s0, n, keys))) {
+        if ((rc = stage_slots(h, s0, n, keys, true))) {
             unmap_keys(h, keys, n);
             return rc;
         }
         pc.mark("stage");
     }
-    rc = put_rows(h, vecs, n, device_src, user_stream, s0);
-    pc.mark("put_rows");
-    if (rc == VSG_OK) rc = build_slots(h, s0, n);
+    rc = build_slots(h, s0, n, cells);
     pc.mark("build_slots");
     if (rc == VSG_OK) {
         const hipError_t e = hipStreamSynchronize(h->stream);

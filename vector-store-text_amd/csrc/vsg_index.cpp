@@ -348,6 +348,7 @@ struct vsg_index {
     // locality launch order (build_slots, f32 rows): pivot rows, the call's cells,
     // partial lists of the pivot search, per-batch sort keys
     uint8_t* d_piv = nullptr;  // PIVOTS x row_bytes, then |row|^2, flags, slot ids, keys
+    uint8_t* d_pivbf = nullptr;  // the pivot rows in bf16 (cells.hip)
     uint32_t* d_cell = nullptr;
     size_t cell_cap = 0;
     float* d_cf32 = nullptr;  // f16 storage: one chunk of rows widened to f32 for the MFMA kernel
@@ -444,6 +445,7 @@ static void free_dev(vsg_index* h) {
     hipFree(h->d_sort_tmp);
     hipFree(h->d_stage);
     hipFree(h->d_piv);
+    hipFree(h->d_pivbf);
     hipFree(h->d_cell);
     hipFree(h->d_cf32);
     hipFree(h->d_cpart_d);
@@ -587,6 +589,7 @@ static size_t loc_chunk(const vsg_index* h, size_t n) {
 static int ensure_locality(vsg_index* h, size_t n, size_t max_b, size_t part_entries, size_t chunk = 0) {
     const size_t rf = loc_row_floats(h);
     if (!h->d_piv) HIP_TRY(dev_alloc(&h->d_piv, LOC_PIVOTS * (rf * 4 + 4 + 1 + 4 + 8) + 256));
+    if (!h->d_pivbf) HIP_TRY(dev_alloc(&h->d_pivbf, cells_pivot_bytes((int)LOC_PIVOTS, (int)rf)));
     if (h->st == ST_F16 && chunk > h->cf32_cap) {
         dfree(h, h->d_cf32);
         h->cf32_cap = 0;
@@ -679,8 +682,11 @@ static int compute_cells(vsg_index* h, uint32_t s0, size_t n, std::vector<uint32
     const size_t P = std::min({LOC_PIVOTS, n, (size_t)env_double("VSG_BUILD_LOCALITY_PIVOTS", 1024)});
     // the f16 pivot rows are staged in the widened-chunk buffer: chunk >= P
     const size_t chunk = std::max(loc_chunk(h, n), P);
+    // bf16 MFMA nearest pivot (cells.hip); VSG_BUILD_CELLS_F32=1: round 2's f32 exact
+    // kernel + top-16 partial lists (same cells up to bf16 near-ties, 6-8x the time)
+    const bool f32 = env_double("VSG_BUILD_CELLS_F32", 0) != 0;
     size_t part_entries = 0;
-    for (size_t c0 = 0; c0 < n; c0 += chunk) {
+    for (size_t c0 = 0; f32 && c0 < n; c0 += chunk) {
         const size_t nq = std::min(chunk, n - c0);
         part_entries = std::max(part_entries, nq * (size_t)cell_shape(nq, P).nparts * 16);
     }
@@ -706,7 +712,13 @@ static int compute_cells(vsg_index* h, uint32_t s0, size_t n, std::vector<uint32
         hipError_t e = hipSuccess;
         const uint8_t* rows = loc_rows(h, (size_t)s0 + c0, nq, st, e);
         HIP_TRY(e);
-        HIP_TRY(rows_to_cells(h, rows, h->d_sqnorm + s0 + c0, nq, P, h->d_cpart_d, h->d_cpart_i, h->d_cell + c0, st));
+        if (f32)
+            HIP_TRY(rows_to_cells(h, rows, h->d_sqnorm + s0 + c0, nq, P, h->d_cpart_d, h->d_cpart_i, h->d_cell + c0,
+                                  st));
+        else
+            HIP_TRY(launch_cells(h->mk, reinterpret_cast<const float*>(pv.rows), pv.sq, (int)P,
+                                 reinterpret_cast<const float*>(rows), nq, (int)loc_row_floats(h), h->d_pivbf,
+                                 c0 == 0, h->d_cell + c0, st));
     }
     return VSG_OK;
 }

@@ -22,7 +22,7 @@ if [ "$STAGE" = all ] || [ "$STAGE" = bench ]; then
   tail -c 600 gpurun_out/r04_bench_n1.log
   EF=${2:-36}
   P=gpurun_out/prof_bench_$(date +%s)  # one directory per run: gpurun merges outputs back
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P -- python3 -u bench.py --no-cpu --upper-ef 0 --rerank-leg 0 --config-ef 0 --ef $EF --steps 10 > gpurun_out/r04_prof_bench.log 2>&1 || exit 1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P -- python3 -u bench.py --no-cpu --upper-ef 0 --rerank-leg 0 --config-ef 0 --streams-leg 0 --ef $EF --steps 10 > gpurun_out/r04_prof_bench.log 2>&1 || exit 1
   find $P -name '*kernel_trace.csv' -size +20M -delete
   echo "rocprof output: $P"
 fi

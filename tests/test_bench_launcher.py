@@ -66,3 +66,24 @@ def test_gpus_4_hybrid_layout():
     assert r["shard_mode"]["shards_per_group"] == 4 and r["shard_mode"]["queries_per_step"] == 1000
     assert r["replica_mode"]["groups"] == 4 and r["replica_mode"]["queries_per_step"] == 4000
     assert r["sharded_abi"]["shards"] == 4
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gpus_1_line_fields():
+    """N = 1 at a small size: the line carries the roofline (frac <= 1), the build
+    roofline, and the 2-stream leg, whose results equal the single-stream steps."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, "-u", BENCH, "--rows", "100000", "--queries", "4000", "--gt-queries", "2000",
+                          "--steps", "4", "--warmup", "1", "--config-ef", "0", "--upper-ef", "0", "--rerank-leg", "0",
+                          "--no-cpu"],
+                         env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [json.loads(s) for s in out.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = lines[0]
+    assert r["n_gpus"] == 1 and r["value"] > 0 and r["config"]["recall_at_10"] >= 0.95
+    assert 0 < r["roofline"]["frac"] <= 1.0 and r["roofline"]["kernel"] == "hnsw_search_reg_kernel"
+    cs = r["concurrent_streams"]
+    assert cs["streams"] == 2 and cs["qps"] > 0 and cs["results_equal_single_stream"] is True
+    assert r["build_vectors_per_s"] > 0

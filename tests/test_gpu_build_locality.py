@@ -1,8 +1,9 @@
 """GPU: the build's locality launch order changes no output.
 
 build_slots (vector-store-text_amd/csrc/vsg_index.cpp) launches the nodes of each
-insert batch grouped by locality cell (nearest of up to 1,024 pivot rows, found by the
-f32 MFMA exact kernel), dealt XCD-contiguously, so that co-resident waves insert
+insert batch grouped by locality cell (nearest of up to 1,024 pivot rows, found on the
+bf16 matrix cores by csrc/cells.hip, or by the f32 MFMA exact kernel with
+VSG_BUILD_CELLS_F32=1), dealt XCD-contiguously, so that co-resident waves insert
 neighbouring vectors and share rows in cache.  Nodes of one batch descend from the same
 graph snapshot, write only their own rows and their own pair range, and the pairs are
 sorted by (level, v, u) before the reverse-link kernel -- so the graph must be the same
@@ -45,10 +46,14 @@ def test_locality_order_same_graph(metric, quant, dim, data, monkeypatch):
     parts = (30_000, 10_000)  # a bulk build, then an append to the non-empty graph
     a = _build(monkeypatch, "0", metric, quant, x, parts)
     b = _build(monkeypatch, "1", metric, quant, x, parts)
+    monkeypatch.setenv("VSG_BUILD_CELLS_F32", "1")
+    c = _build(monkeypatch, "1", metric, quant, x, parts)
+    monkeypatch.delenv("VSG_BUILD_CELLS_F32")
     ga, gb = a.export(), b.export()
     assert (ga["entry"], ga["max_level"]) == (gb["entry"], gb["max_level"])
     for f in ("levels", "adj0", "upper_off", "upper", "keys"):
         np.testing.assert_array_equal(ga[f], gb[f], err_msg=f)
+        np.testing.assert_array_equal(ga[f], c.export()[f], err_msg=f + " (f32 cells)")
     sa, sb = a.stats(), b.stats()
     for f in ("build_distances", "build_adjacency", "build_batches"):
         assert sa[f] == sb[f], f
@@ -85,3 +90,34 @@ def test_split_insert_same_graph(metric, quant, dim, M, efc, monkeypatch):
     sa, sb = a.stats(), b.stats()
     for f in ("build_distances", "build_adjacency", "build_select_distances"):
         assert sa[f] == sb[f], f
+
+
+def test_staging_and_rejected_call_leave_the_same_graph(monkeypatch):
+    """add() enqueues the rows and the locality cells before it maps the keys (their
+    slots lie beyond the index's size), and stages its uploads in pinned memory up to
+    VSG_PIN_MAX: a call rejected for a duplicate key changes nothing -- the next add
+    builds the graph of an index that never saw it -- and pageable staging
+    (VSG_PIN_MAX=0) builds the same graph as pinned."""
+    n, dim = 30_000, 96
+    x = G.clustered(n + 5_000, dim, 71, 72)
+    monkeypatch.setenv("VSG_BUILD_LOCALITY_MIN", "256")
+
+    def build(pin, reject):
+        monkeypatch.setenv("VSG_PIN_MAX", pin)
+        idx = vsg.Index(dim, "l2sq", "f32", 16, 96, 64, seed=9)
+        idx.add(np.arange(20_000), x[:20_000])
+        if reject:
+            keys = np.arange(20_000, 25_000)
+            keys[-1] = 5  # already in the index
+            with pytest.raises(vsg.VsgError):
+                idx.add(keys, x[20_000:25_000] + 1.0)
+            assert idx.size() == 20_000
+        idx.add(np.arange(20_000, n), x[20_000:n])
+        return idx
+
+    ref = build(str(512 << 20), False).export()
+    for pin, reject in (("0", False), (str(512 << 20), True), ("0", True)):
+        g = build(pin, reject).export()
+        assert (g["entry"], g["max_level"]) == (ref["entry"], ref["max_level"])
+        for f in ("levels", "adj0", "upper_off", "upper", "keys"):
+            np.testing.assert_array_equal(g[f], ref[f], err_msg=f"{f} pin={pin} reject={reject}")

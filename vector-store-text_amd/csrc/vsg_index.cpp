@@ -796,16 +796,26 @@ static int map_keys(vsg_index* h, const uint64_t* keys, size_t n, uint32_t s0) {
 // offsets (the upper table is sized for the whole call here, so the build never
 // reallocates it), keys, flags and upper_off uploaded; `slots` grows.  No link
 // to the new rows exists yet, so searches cannot reach them.
-// grow a pinned host staging buffer (its previous contents are not kept)
+// Host staging of an add's uploads: pinned (grown, contents not kept) up to
+// PIN_MAX bytes; a larger call stages in `fallback` (pageable: its copies block
+// the host until the stream reaches them, a few ms against that call's seconds)
+// (VSG_PIN_MAX overrides the 512 MiB, e.g. 0 in the tests of the pageable path)
+static size_t pin_max() { return (size_t)env_double("VSG_PIN_MAX", (double)((size_t)512 << 20)); }
 static int ensure_pinned(uint8_t** p, size_t& cap, size_t need) {
-    if (need <= cap) return VSG_OK;
-    const size_t want = std::max(need, cap * 2);
+    const size_t pmax = pin_max();
+    if (need <= cap || need > pmax) return VSG_OK;
+    const size_t want = std::min(pmax, std::max(need, cap * 2));
     if (*p) (void)hipHostFree(*p);
     *p = nullptr;
     cap = 0;
     HIP_TRY(hipHostMalloc((void**)p, want, hipHostMallocDefault));
     cap = want;
     return VSG_OK;
+}
+static uint8_t* staging(uint8_t* pinned, size_t cap, size_t need, std::vector<uint8_t>& fallback) {
+    if (need <= cap && need <= pin_max()) return pinned;
+    fallback.resize(need);
+    return fallback.data();
 }
 
 // Levels of slots [s0, s0 + n) (a pure function of seed and slot) and the upper
@@ -830,7 +840,8 @@ static int stage_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* keys
     // behind the locality cells without blocking the host
     int rc0 = ensure_pinned(&h->h_stg, h->h_stg_cap, n * 12 + 64);
     if (rc0) return rc0;
-    uint64_t* kst = reinterpret_cast<uint64_t*>(h->h_stg);
+    std::vector<uint8_t> big;
+    uint64_t* kst = reinterpret_cast<uint64_t*>(staging(h->h_stg, h->h_stg_cap, n * 12 + 64, big));
     uint32_t* upper_off = reinterpret_cast<uint32_t*>(kst + n);
     std::memcpy(kst, keys, n * 8);
     // levels and upper rows
@@ -904,7 +915,8 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
     // spatially coherent (a cluster-sorted input otherwise wrecks the graph).
     // order | pair_off | list_off (n x u32 each) | blev (n x i8), in pinned memory
     if ((rc = ensure_pinned(&h->h_plan, h->h_plan_cap, n * 13 + 64))) return rc;
-    uint32_t* order = reinterpret_cast<uint32_t*>(h->h_plan);
+    std::vector<uint8_t> big;
+    uint32_t* order = reinterpret_cast<uint32_t*>(staging(h->h_plan, h->h_plan_cap, n * 13 + 64, big));
     uint32_t* pair_off = order + n;
     uint32_t* list_off = pair_off + n;
     int8_t* blev = reinterpret_cast<int8_t*>(list_off + n);
@@ -1395,7 +1407,7 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
     // pinned staging first: hipHostMalloc waits for the device, so it must not
     // come after the cells (stage_slots / build_slots only find it sized)
     if ((rc = ensure_pinned(&h->h_stg, h->h_stg_cap, n * 12 + 64)) ||
-        (rc = ensure_pinned(&h->h_plan, h->h_plan_cap, n * 13 + 64)))
+        (!(h->opt.flags & VSG_FLAG_EXACT_ONLY) && (rc = ensure_pinned(&h->h_plan, h->h_plan_cap, n * 13 + 64))))
         return rc;
     if ((rc = put_rows(h, vecs, n, device_src, user_stream, s0))) return rc;
     pc.mark("put_rows");

@@ -5,7 +5,8 @@
 // f32 exact kernel + top-16 partial lists it replaced (C2: ~18 ms per 1M-row add).
 //
 // One wave = 32 rows (the B operand, N) against pivot groups of 256 (eight
-// 32-pivot A tiles, 8 x 16 accumulators); K = the padded row in steps of 16.
+// 32-pivot A tiles, 8 x 16 accumulators); K = the padded row in steps of 16; a
+// block's 4 waves share each pivot chunk through LDS.
 // Lane l holds row (l % 32) of every C tile and 16 of each tile's pivots, keeps
 // its own best (distance, pivot) and the two half-waves combine at the end.
 // Rows stay f32 in HBM and are rounded to bf16 as they are loaded; pivots are
@@ -40,36 +41,64 @@ __global__ __launch_bounds__(256) void pivots_bf16_kernel(const float* __restric
     }
 }
 
+// The pivots of a pass are shared by the block's 4 waves through LDS: 32-dim
+// chunks (256 pivots x 64 B, rows padded to 80 B so the 16 lanes of a ds_read_b128
+// hit distinct 16-B slots), double-buffered, one barrier per chunk -- each pivot
+// byte leaves L2 once per 128 rows instead of once per 32.
+constexpr int CELL_PROW = 40;  // bf16 per padded LDS pivot row (32 + 8)
+
 template <int MET>
 __global__ __launch_bounds__(256, 2) void cells_kernel(const uint4* __restrict__ pb, const float* __restrict__ psq,
                                                        int P, int Ppad, const float* __restrict__ rows, size_t nrows,
                                                        int D, uint32_t* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const size_t r0 = ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 32;
-    if (r0 >= nrows) return;
+    __shared__ __attribute__((aligned(16))) uint16_t sp[2][32 * CELL_GROUP * CELL_PROW];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const size_t r0 = ((size_t)blockIdx.x * 4 + (tid >> 6)) * 32;
+    const bool live = r0 < nrows;  // every wave takes part in the block's barriers
     const int n = lane & 31, kb = lane >> 5;
-    const size_t row = min(r0 + (size_t)n, nrows - 1);
+    const size_t row = live ? min(r0 + (size_t)n, nrows - 1) : 0;
     const float* xr = rows + row * (size_t)D + 8 * kb;
-    const int dq = D / 8;  // 16-B (8 x bf16) pieces per pivot row
+    const int dq = D / 8;  // 16-B pieces per pivot row
+    const int nch = D / 32;
     float best = __builtin_inff();
     uint32_t bid = 0xFFFFFFFFu;
+    // chunk c of pass t0 -> buffer: 256 pivots x 4 pieces, 4 per thread
+    auto stage = [&](int t0, int c, uint16_t* dst) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + 256 * u;  // (pivot, piece)
+            const int pv = e >> 2, pc = e & 3;
+            const uint4 v = pb[(size_t)(t0 + pv) * dq + (size_t)c * 4 + pc];
+            *reinterpret_cast<uint4*>(dst + pv * CELL_PROW + pc * 8) = v;
+        }
+    };
     for (int t0 = 0; t0 < Ppad; t0 += 32 * CELL_GROUP) {
         cfloatx16 acc[CELL_GROUP];
 #pragma unroll
         for (int t = 0; t < CELL_GROUP; ++t)
 #pragma unroll
             for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
-        const uint4* pa = pb + (size_t)(t0 + n) * dq + kb;
-        for (int k = 0; k < D; k += 16) {
-            const float4 x0 = *reinterpret_cast<const float4*>(xr + k);
-            const float4 x1 = *reinterpret_cast<const float4*>(xr + k + 4);
-            const uint4 xb = make_uint4(pack_bf16(x0.x, x0.y), pack_bf16(x0.z, x0.w), pack_bf16(x1.x, x1.y),
-                                        pack_bf16(x1.z, x1.w));
-            const bf16x8 b = __builtin_bit_cast(bf16x8, xb);
+        __syncthreads();  // the previous pass's last reads of sp[0] are done
+        stage(t0, 0, sp[0]);
+        for (int c = 0; c < nch; ++c) {
+            __syncthreads();  // chunk c in sp[c & 1]; sp[(c + 1) & 1] free
+            if (c + 1 < nch) stage(t0, c + 1, sp[(c + 1) & 1]);
+            const uint16_t* cur = sp[c & 1];
 #pragma unroll
-            for (int t = 0; t < CELL_GROUP; ++t) {
-                const uint4 pv = pa[(size_t)t * 32 * dq + k / 8];
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, pv), b, acc[t], 0, 0, 0);
+            for (int kk = 0; kk < 2; ++kk) {
+                const int k = c * 32 + kk * 16;
+                const float4 x0 = *reinterpret_cast<const float4*>(xr + k);
+                const float4 x1 = *reinterpret_cast<const float4*>(xr + k + 4);
+                const uint4 xb = make_uint4(pack_bf16(x0.x, x0.y), pack_bf16(x0.z, x0.w), pack_bf16(x1.x, x1.y),
+                                            pack_bf16(x1.z, x1.w));
+                const bf16x8 b = __builtin_bit_cast(bf16x8, xb);
+#pragma unroll
+                for (int t = 0; t < CELL_GROUP; ++t) {
+                    const uint4 pv =
+                        *reinterpret_cast<const uint4*>(cur + (t * 32 + n) * CELL_PROW + kk * 16 + kb * 8);
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, pv), b, acc[t], 0, 0, 0);
+                }
             }
         }
         // C[m = pivot][n = row]: register g of lane l holds pivot 8 (g / 4) + 4 (l / 32) + g % 4
@@ -91,14 +120,14 @@ __global__ __launch_bounds__(256, 2) void cells_kernel(const uint4* __restrict__
     const float ob = __shfl_xor(best, 32);
     const uint32_t oi = (uint32_t)__shfl_xor((int)bid, 32);
     if (ob < best || (ob == best && oi < bid)) bid = oi;
-    if (kb == 0 && r0 + n < nrows) out[r0 + n] = bid;
+    if (live && kb == 0 && r0 + n < nrows) out[r0 + n] = bid;
 }
 
 size_t cells_pivot_bytes(int P, int D) { return (size_t)((P + 255) / 256 * 256) * D * 2; }
 
 hipError_t launch_cells(MetricKind mk, const float* piv, const float* psq, int P, const float* rows, size_t nrows,
                         int D, void* pb_scratch, bool convert, uint32_t* out, hipStream_t s) {
-    if (P <= 0 || D % 16 || nrows == 0) return P <= 0 || D % 16 ? hipErrorInvalidValue : hipSuccess;
+    if (P <= 0 || D % 32 || nrows == 0) return P <= 0 || D % 32 ? hipErrorInvalidValue : hipSuccess;
     const int Ppad = (P + 255) / 256 * 256;
     uint32_t* pb = reinterpret_cast<uint32_t*>(pb_scratch);
     if (convert) {

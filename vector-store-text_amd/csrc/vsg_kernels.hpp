@@ -217,7 +217,7 @@ hipError_t launch_gather_rows(const uint8_t* vecs, const float* sqnorm, const ui
 // locality cells (build launch order): out[r] = the nearest of the partial-list
 // entries of row r (MFMA exact search of the rows against pivot rows)
 // locality cells (cells.hip): out[r] = the nearest of P pivot rows (P x D f32,
-// |p|^2 in psq for l2sq) for nrows f32 rows of D floats (D % 16 == 0), on bf16
+// |p|^2 in psq for l2sq) for nrows f32 rows of D floats (D % 32 == 0), on bf16
 // MFMA.  pb_scratch holds cells_pivot_bytes(P, D); convert = (re)fill it from piv.
 size_t cells_pivot_bytes(int P, int D);
 hipError_t launch_cells(MetricKind mk, const float* piv, const float* psq, int P, const float* rows, size_t nrows,

@@ -160,7 +160,10 @@ int vsg_index_set_upper_ef(vsg_index_t* index, size_t upper_ef);
  * completion event, and a writer that frees or rewrites memory the search may
  * read (capacity growth, compaction, the f16 copy's reallocation) first waits
  * for every such event; appends and removes do not wait (the search sees a
- * prefix of them, as with vsg_index_search). */
+ * prefix of them, as with vsg_index_search).  Searches enqueued on different
+ * streams run concurrently on the device (each takes its own scratch set, up
+ * to 4 per index), so a second stream fills the tail of a batch's last round
+ * of resident waves; on one stream they run in order. */
 int vsg_index_search_device(vsg_index_t* index, const float* queries_device, size_t nq, size_t k,
                             size_t ef, uint64_t* out_keys_device, float* out_distances_device,
                             uint32_t* out_counts_device, void* stream);

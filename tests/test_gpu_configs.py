@@ -7,11 +7,13 @@ exactly the per-rank index of bench.py's shard leg.  Every query is searched on 
 shard and the per-shard top-k rows are merged by the HIP merge kernel (the step after
 the RCCL all-gather).  Checks: merged exact top-k == one exact-only index over all 10M
 rows (bit-exact keys and distances); merged HNSW recall@10 >= 0.95 at the per-shard ef
-the 8-shard emulation needs (32, profiles/r01_c3_8shard_emulation_1gpu*.jsonl).
+the 8-shard emulation needs (32, profiles/r01_c3_8shard_emulation_1gpu*.jsonl); the merged
+exact lists of 16 queries against the oracle run shard by shard over all 10M rows.
 
 C5 (configs[4]): 1M x 1536 f32 inner product, batched brute force on the f32 matrix
 cores (mfma_exact.hip, `v_mfma_f32_32x32x2_f32`).  Bit-exact against the oracle at
-1536-d on integer data; at full size MFMA == VALU exact kernel up to near-ties.
+1536-d on integer data; at full size MFMA == VALU exact kernel up to near-ties, and the
+B=64 MFMA tile == the oracle on float data (distances within 1e-5, keys up to near-ties).
 """
 import numpy as np
 import pytest
@@ -28,6 +30,21 @@ def recall(found, truth, k):
                           for i in range(truth.shape[0])]))
 
 
+def assert_topk_matches_oracle(gk, gd, ok, od, tol=1e-5):
+    """GPU f32 top-k vs the oracle's on float data: accumulation orders differ, so
+    distances agree within `tol` (relative, floor 1) and a key may differ only where
+    the oracle's own distances tie within `tol` at that rank or at the k-th."""
+    scale = np.maximum(1.0, np.abs(od))
+    assert np.max(np.abs(gd - od) / scale) < tol
+    for i in range(ok.shape[0]):
+        if np.array_equal(gk[i], ok[i]):
+            continue
+        kth = od[i, -1]
+        for j in np.flatnonzero(gk[i] != ok[i]):
+            near = np.abs(od[i] - od[i, j]) / scale[i] < tol
+            assert near.sum() > 1 or abs(od[i, j] - kth) / scale[i, j] < tol, (i, j)
+
+
 def test_c3_10m768_cos_eight_row_shards_merged():
     import torch
     n, dim, shards, nq, k = 10_000_000, 768, 8, 1000, 10
@@ -36,6 +53,8 @@ def test_c3_10m768_cos_eight_row_shards_merged():
     full = vsg.Index(dim, "cos", "f32", exact_only=True)
     full.reserve(n)
     parts = []
+    qh = q[:16].cpu().numpy()
+    ork, ord_ = [], []  # oracle per shard on 16 queries: pins the merged exact at size
     for s in range(shards):
         lo, hi = s * n // shards, (s + 1) * n // shards
         x = vsg.datagen_device("clustered", hi - lo, dim, bs, ms, start=lo)
@@ -45,6 +64,9 @@ def test_c3_10m768_cos_eight_row_shards_merged():
         idx.add_device(keys, x)
         full.add_device(keys, x)
         torch.cuda.synchronize()
+        sk, sd, _ = O.exact_search("cos", x.cpu().numpy(), qh, k, keys=keys, threads=16)
+        ork.append(sk)
+        ord_.append(sd)
         del x
         parts.append(idx)
     assert sum(p.size() for p in parts) == n and full.size() == n
@@ -58,6 +80,11 @@ def test_c3_10m768_cos_eight_row_shards_merged():
     tk, td = full.search_device(q, k, exact=True)
     np.testing.assert_array_equal(ek, tk.cpu().numpy().view(np.uint64))
     np.testing.assert_array_equal(ed, td.cpu().numpy())
+    # oracle at full size: merge the per-shard oracle lists by (distance, key)
+    ak, ad = np.concatenate(ork, axis=1), np.concatenate(ord_, axis=1)
+    o = np.lexsort((ak, ad), axis=1)[:, :k]
+    assert_topk_matches_oracle(ek[:16], ed[:16], np.take_along_axis(ak, o, 1),
+                               np.take_along_axis(ad, o, 1))
     r = {ef: recall(merged(ef)[0], ek, k) for ef in (16, 32, 64)}
     print("C3 8-shard merged recall@10 by per-shard ef:", r)
     assert r[32] >= 0.95 and r[64] >= r[32] - 0.002
@@ -93,6 +120,7 @@ def test_c5_1m1536_ip_mfma_vs_valu_full_size(nq, monkeypatch):
     idx = vsg.Index(dim, "ip", "f32", exact_only=True)
     idx.reserve(n)
     idx.add_device(np.arange(n, dtype=np.uint64), x)
+    xh = x.cpu().numpy() if nq == 64 else None
     del x
     res = {}
     for mfma in ("1", "0"):
@@ -108,3 +136,6 @@ def test_c5_1m1536_ip_mfma_vs_valu_full_size(nq, monkeypatch):
         assert np.min(np.diff(vd[i])) / scale[i].max() < 1e-5 or set(mk[i, :k]) == set(vk[i, :k]), i
     assert same.mean() >= 0.98
     assert np.all(np.diff(md[:, :k], axis=1) >= 0)
+    if xh is not None:  # the MFMA tile of B=64 against the oracle at full size
+        ok, od, _ = O.exact_search("ip", xh, q.cpu().numpy(), k, threads=16)
+        assert_topk_matches_oracle(mk[:, :k], md[:, :k], ok, od)

@@ -98,6 +98,9 @@ def parse():
                          "devices in rank 0's process (include/vsg.h vsg_sharded_*), peer-DMA gather + HIP merge")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse several ranks on one GPU (collectives via host)")
+    ap.add_argument("--host-abi-leg", type=int, default=1,
+                    help="N=1: also time the drop-in's host-buffer ABI -- build via vsg_index_add from host f32 "
+                         "rows, QPS via vsg_index_search from host queries (PCIe included) -- beside `value`")
     return ap.parse_args()
 
 
@@ -572,6 +575,10 @@ def main():
             except Exception as e:  # noqa: BLE001
                 out["sharded_abi"] = {"error": f"{type(e).__name__}: {e}"[:400]}
         c.barrier()
+    # the host-buffer drop-in ABI at N=1 (vsg_index_add / vsg_index_search take host
+    # memory, as usearch's add(key, &[f32]) and search(&[f32], k) do, usearch.rs:221, 276)
+    if world == 1 and a.host_abi_leg and a.mode == "hnsw":
+        out["host_abi"] = host_abi_leg(c, head)
     # CPU baseline (rank 0, N=1 only): oracle/ restatement of usearch
     if world == 1 and rank == 0 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(a, head["index"], head["q"], head["ef"], head["x"], head["gt"])
@@ -756,6 +763,67 @@ def abi_leg(c):
     return res
 
 
+def host_abi_leg(c, head):
+    """N=1, beside `value`: the reference's own call shapes through the C ABI with host
+    buffers (PCIe included).  Build: a fresh index filled by vsg_index_add from host f32
+    rows (the rows `value`'s index was built from, copied out of HBM first, untimed).
+    Search: vsg_index_search with host queries / host outputs over the headline index at
+    the headline ef, K steps; results compared with the device-resident search."""
+    import torch
+
+    import vsg
+
+    a = c.a
+    xh = head["x"].cpu().numpy()
+    qh = head["q"].cpu().numpy()
+    idx = vsg.Index(a.dim, a.metric, a.quant, a.M, a.efc, 128, device=c.local, seed=0x5EED)
+    idx.reserve(a.rows)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    idx.add(np.arange(a.rows, dtype=np.uint64), xh)
+    build_s = time.perf_counter() - t0
+    del xh
+    ef, index = head["ef"], head["index"]
+    ng = head["gt"].shape[0]
+    rb = recall_np(idx.search(qh[:ng], a.k, ef).keys, head["gt"], a.k)
+    idx.close()
+    for _ in range(max(1, a.warmup)):
+        m = index.search(qh, a.k, ef)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        m = index.search(qh, a.k, ef)
+    el = time.perf_counter() - t0
+    dk, dd = index.search_device(head["q"], a.k, ef)
+    same = bool(np.array_equal(dk.cpu().numpy().view(np.uint64), m.keys) and np.array_equal(dd.cpu().numpy(), m.distances))
+    return {"build_vectors_per_s": round(a.rows / build_s, 1), "build_seconds": round(build_s, 3),
+            "build_recall_at_10": round(rb, 4),
+            "qps": round(a.queries * a.steps / el, 1), "ms_per_step": round(1000.0 * el / a.steps, 3), "ef": ef,
+            "results_equal_device_search": same,
+            "note": "vsg_index_add from host f32 rows (a fresh index of the same rows, PCIe included) and "
+                    "vsg_index_search with host queries and outputs over the headline index (PCIe both ways): "
+                    "the reference's add(key, &[f32]) / search(&[f32], k) call shapes, batched"}
+
+
+def recall_np(found, gt, k):
+    f = np.asarray(found).astype(np.int64)
+    g = np.asarray(gt).astype(np.int64)
+    n = min(len(f), len(g))
+    return float((f[:n, :k, None] == g[:n, None, :k]).any(axis=1).sum(axis=1).mean() / k)
+
+
+def kernel_src_sha() -> str:
+    """sha256 over the library sources (vector-store-text_amd/csrc): a PMC summary
+    is used only while the kernels it profiled are the ones in this tree."""
+    import hashlib
+    d = os.path.join(ROOT, "vector-store-text_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".hpp", ".cpp")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def build_roofline(a, head):
     """The build against the HBM roofline on DEVICE time (HIP events around every
     batch's launches on the build stream, vsg_stats_t.build_*_ns).  Dominant kernel:
@@ -786,7 +854,7 @@ def build_roofline(a, head):
         d = json.load(open(os.path.join(ROOT, "profiles", "build_pmc.json")))
         w = d.get("workload", {})
         if (w.get("n"), w.get("dim"), w.get("metric"), w.get("M"), w.get("efc"), w.get("forward_links")) == (
-                head["nloc"], a.dim, a.metric, a.M, a.efc, "M"):
+                head["nloc"], a.dim, a.metric, a.M, a.efc, "M") and d.get("kernel_src_sha") == kernel_src_sha():
             pmc = d
     except (OSError, ValueError):
         pass
@@ -829,6 +897,9 @@ def pmc_traffic(a, ef):
     # (round 4); earlier summaries profiled the M0-forward graph
     if (w.get("n"), w.get("dim"), w.get("queries"), w.get("ef"), w.get("metric"), w.get("forward_links")) != (
             a.rows, a.dim, a.queries, ef, a.metric, "M"):
+        return None
+    # profiled kernels must be this tree's (the summary records the source hash it ran)
+    if d.get("kernel_src_sha") != kernel_src_sha():
         return None
     return d.get("hbm_bytes_per_launch")
 

@@ -60,6 +60,11 @@ extern "C" {
  * are the f32 metric values; the candidate set can differ from an f32 walk.
  * No usearch equivalent (opt-in; f32 storage only). */
 #define VSG_FLAG_F16_TRAVERSAL 2u
+/* flags: append-only adds -- removed slots stay tombstones until
+ * vsg_index_compact (round-4 behaviour) instead of being re-linked by the next
+ * adds (usearch's free-slot reuse, vsg_index_add).  Exact-only indexes are
+ * always append-only. */
+#define VSG_FLAG_NO_SLOT_REUSE 4u
 
 typedef struct vsg_index vsg_index_t;
 
@@ -98,9 +103,19 @@ typedef struct {
     uint64_t build_sort_ns;            /*   stream): insert (descent + beam + selection), pair sort, */
     uint64_t build_reverse_ns;         /*   reverse links -- the build roofline's time base */
     uint64_t build_select_ns;          /* the selection kernel's share of build_insert_ns (split insert) */
-    uint64_t search_filter_overflow;   /* filtered searches (index with removed entries): candidates
-                                          dropped for want of room in the candidate set; results are
-                                          usearch's exactly while this stays 0 */
+    uint64_t search_filter_overflow;   /* filtered searches (index with removed entries): queries whose
+                                          candidate set (registers / LDS list) ran out of room ... */
+    uint64_t search_filter_reruns;     /* ... and were searched again on a list in device memory sized
+                                          for every slot: results are usearch's either way */
+    uint64_t slots_reused;             /* removed slots re-linked by adds (free-slot reuse) */
+    uint64_t ktile_copy_failures;      /* exact-only adds whose K-tiled copy failed (completed by the
+                                          next exact search; the add itself succeeded) */
+    uint64_t host_searches;            /* host-buffer searches (vsg_index_search / _exact_search) ... */
+    uint64_t host_search_ns;           /* ... their wall time inside the library, and with
+                                          VSG_PROFILE_HOST_SEARCH=1 the device-timeline split of it: */
+    uint64_t host_h2d_ns;              /*   query upload, */
+    uint64_t host_device_ns;           /*   search kernels (prepare .. merge), */
+    uint64_t host_d2h_ns;              /*   result download (HIP events on the call's stream) */
 } vsg_stats_t;
 
 /* replaces usearch::Index::new(&options) — src/index/usearch.rs:98 */
@@ -120,15 +135,29 @@ int vsg_index_contains(const vsg_index_t* index, uint64_t key);
  * Batched: n vectors of `dimensions` f32, row-major.  Any live duplicate
  * (or a duplicate inside the batch) => VSG_EDUPKEY and nothing is inserted.
  * Grows capacity automatically when needed (the reference reserves ahead,
- * usearch.rs:200-212; growth here is the same operation). */
+ * usearch.rs:200-212; growth here is the same operation).
+ * Free-slot reuse (usearch index_dense: add_ pops free_keys_ and runs
+ * index_gt::update on the slot): the first keys of the call take removed slots,
+ * oldest removal first (the entry point's slot is skipped while it is the entry
+ * point); such a slot keeps its level and the other nodes' links into it, gets
+ * the new key and vector and is re-linked in place, before the rest of the call
+ * is appended.  The reference's replace is remove + add (usearch.rs:214-221), so
+ * an upsert stream recycles slots instead of growing.  Rules in
+ * oracle/vsg_oracle.h orc_hnsw_add; VSG_FLAG_NO_SLOT_REUSE turns it off. */
 int vsg_index_add(vsg_index_t* index, const uint64_t* keys, const float* vectors, size_t n);
 /* Same, with `vectors` already in device memory (f32, n x dimensions). */
 int vsg_index_add_device(vsg_index_t* index, const uint64_t* keys, const float* vectors_device,
                          size_t n, void* stream);
 
 /* replaces usearch::Index::remove(key) — src/index/usearch.rs:215, :245.
- * Tombstones; *n_removed (optional) counts keys that were live. */
+ * Tombstones (traversed by searches, never returned) and queues each slot at
+ * the back of the free ring for reuse by later adds; *n_removed (optional)
+ * counts keys that were live. */
 int vsg_index_remove(vsg_index_t* index, const uint64_t* keys, size_t n, size_t* n_removed);
+/* The free ring (usearch index_dense free_keys_): removed slots, oldest removal
+ * first -- exactly the index's removed slots.  Copies up to `cap` slot ids to
+ * `out` (may be NULL) and returns how many there are. */
+size_t vsg_index_free_slots(const vsg_index_t* index, uint32_t* out, size_t cap);
 
 /* replaces usearch::Index::search(&[f32], k) — src/index/usearch.rs:275-277.
  * HNSW k-NN for nq queries; ef = max(ef ? ef : expansion_search, k).
@@ -196,8 +225,9 @@ int vsg_index_import(vsg_index_t* index, size_t slots, const float* vectors,
                      const uint32_t* adj0, const uint32_t* upper_off, const uint32_t* upper,
                      size_t upper_rows, uint32_t entry, int max_level);
 
-/* Compaction: tombstoned rows (vsg_index_remove) keep
- * routing the traversal until compaction drops them.  Gathers the live rows in
+/* Compaction (optional since round 5: adds re-link removed
+ * slots): tombstoned rows (vsg_index_remove) keep routing the traversal until
+ * the next adds reuse them or compaction drops them.  Gathers the live rows in
  * slot order into a dense image and rebuilds the graph over them on the GPU.
  * Keys, live size and capacity are unchanged; *n_dropped (optional) = slots
  * freed.  Takes the writer lock.  usearch compacts through its own
@@ -206,9 +236,10 @@ int vsg_index_compact(vsg_index_t* index, size_t* n_dropped);
 
 /* Persistence (the reference rebuilds from a DB scan instead,
  * src/db_index.rs:213-237).  One file: a 128-byte header (magic "VSGIDX\0\1",
- * version 1, options, sizes, entry point, FNV-1a-64 checksums) followed by the
+ * version 2, options, sizes, entry point, FNV-1a-64 checksums) followed by the
  * HBM image (stored rows, |x|^2, keys, flags, levels, level-0 adjacency,
- * upper_off, upper rows).  Save writes `path`.tmp then renames.  Load creates a
+ * upper_off, upper rows) and the free ring ((slots - live) u32, oldest removal
+ * first).  Version-1 files (no ring) load with the removed slots ascending.  Save writes `path`.tmp then renames.  Load creates a
  * new index on `device` and verifies sizes and both checksums; a loaded index
  * answers searches bit-identically to the saved one. */
 typedef struct {
@@ -316,7 +347,8 @@ typedef struct {
     uint32_t max_batch;         /* messages drained per worker wake-up; 0 => 65536 */
     uint32_t max_wait_us;       /* optional coalescing window; 0 => natural batching */
     uint32_t compact_percent;   /* vsg_index_compact once tombstones >= this % of stored
-                                   rows; 0 => 50, >= 100 => never */
+                                   rows; 0 => never (default since round 5: adds re-link
+                                   removed slots, as usearch does), >= 100 => never */
     uint32_t concurrent_reads;  /* n >= 1: anns run on n read workers beside the writes and see
                                    a prefix of them (the reference's fire-and-forget adds,
                                    usearch.rs:200-221); n >= 2 keeps n search batches in
@@ -330,6 +362,11 @@ typedef struct {
     uint64_t add_errors, remove_errors, search_errors;
     uint64_t max_search_batch, max_add_batch;
     uint64_t compactions, compacted_rows, compact_errors;
+    /* serving-path breakdown, steady-clock ns summed: per ann, submission -> its batch
+     * starts (coalescing / queueing) and finish -> the caller running again (wake-up);
+     * per search batch (search_calls of them), the batched search call and the
+     * result copies + completion signals */
+    uint64_t ann_queue_ns, ann_wake_ns, batch_search_ns, batch_notify_ns;
 } vsg_actor_counters_t;
 
 /* replaces usearch::new (the actor spawn + Index::new + reserve(1M)) — usearch.rs:82-139 */

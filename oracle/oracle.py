@@ -57,6 +57,9 @@ def lib():
         L.orc_hnsw_add.argtypes = [P, P, P, sz, C.c_int]
         L.orc_hnsw_remove.restype = sz
         L.orc_hnsw_remove.argtypes = [P, P, sz]
+        L.orc_hnsw_free_list.restype = sz
+        L.orc_hnsw_free_list.argtypes = [P, P, sz]
+        L.orc_hnsw_set_slot_reuse.argtypes = [P, C.c_int]
         L.orc_hnsw_search.argtypes = [P, P, sz, sz, sz, P, P, P, C.c_int, P]
         L.orc_hnsw_entry.argtypes = [P, P, P]
         L.orc_hnsw_export.argtypes = [P] * 8
@@ -152,6 +155,16 @@ class HnswOracle:
     def remove(self, keys):
         keys = np.ascontiguousarray(keys, np.uint64)
         return lib().orc_hnsw_remove(self.h, _p(keys), len(keys))
+
+    def free_list(self):
+        """The free ring (usearch index_dense free_keys_), oldest removal first."""
+        n = lib().orc_hnsw_free_list(self.h, None, 0)
+        out = np.empty(n, np.uint32)
+        lib().orc_hnsw_free_list(self.h, _p(out), n)
+        return out
+
+    def set_slot_reuse(self, on: bool) -> None:
+        lib().orc_hnsw_set_slot_reuse(self.h, 1 if on else 0)
 
     def search(self, queries, k, ef=0, threads=0, return_ndist=False):
         queries = np.ascontiguousarray(queries, np.float32).reshape(-1, self.dim)

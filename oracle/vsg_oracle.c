@@ -307,6 +307,11 @@ struct orc_hnsw {
     pthread_mutex_t* node_locks;
     pthread_mutex_t global_lock;
     keymap km;
+    /* usearch index_dense free_keys_: removed slots, oldest removal first
+     * (ring[0] is the next to reuse); exactly the removed slots */
+    uint32_t* ring;
+    size_t ring_n, ring_cap;
+    int reuse; /* 0: append-only adds (orc_hnsw_set_slot_reuse) */
     void* sscr; /* cached search scratch (scratch_t[sscr_n]) */
     int sscr_n;
     size_t sscr_slots, sscr_ef;
@@ -337,6 +342,7 @@ orc_hnsw* orc_hnsw_new(size_t dim, int metric, size_t connectivity, size_t expan
     h->seed = seed;
     h->entry = ORC_EMPTY;
     h->max_level = -1;
+    h->reuse = 1;
     pthread_mutex_init(&h->global_lock, NULL);
     km_init(&h->km, 1024);
     return h;
@@ -357,6 +363,7 @@ void orc_hnsw_free(orc_hnsw* h) {
     free(h->adj0);
     free(h->upper_off);
     free(h->upper);
+    free(h->ring);
     km_free(&h->km);
     pthread_mutex_destroy(&h->global_lock);
     free(h);
@@ -464,7 +471,7 @@ static size_t read_row(const orc_hnsw* h, uint32_t s, int l, uint32_t* out, int 
 /* usearch search_for_one_ (upper levels): greedy move to the closest
  * neighbour until no neighbour improves; ties by slot. */
 static uint32_t greedy(const orc_hnsw* h, const float* q, uint32_t ep, float* dep, int l,
-                       scratch_t* s, int locked) {
+                       scratch_t* s, int locked, uint32_t self) {
     uint32_t cur = ep;
     float dcur = *dep;
     for (;;) {
@@ -473,6 +480,7 @@ static uint32_t greedy(const orc_hnsw* h, const float* q, uint32_t ep, float* de
         float dbest = dcur;
         for (size_t i = 0; i < c; ++i) {
             uint32_t n = s->nbr[i];
+            if (n == self) continue; /* a node is never its own candidate */
             float d = orc_distance(h->metric, q, VEC(h, n), h->dim);
             s->ndist++;
             if (cand_less(d, n, dbest, best)) {
@@ -493,8 +501,11 @@ static uint32_t greedy(const orc_hnsw* h, const float* q, uint32_t ep, float* de
  * equivalent to the two-heap formulation (a candidate evicted from the top
  * list can never be closer than the list's worst again). Returns list size. */
 static size_t beam(const orc_hnsw* h, const float* q, uint32_t ep, float dep, size_t ef, int l,
-                   scratch_t* s, int locked) {
+                   scratch_t* s, int locked, uint32_t self) {
     scratch_newgen(s);
+    /* the node being (re)linked is never its own candidate: a reused slot is
+     * reachable through other nodes' kept links into it */
+    if (self != ORC_EMPTY) s->stamp[self] = s->gen;
     cand_t* L = s->list;
     uint8_t* X = s->expanded;
     size_t n = 1;
@@ -673,8 +684,13 @@ static void add_reverse(orc_hnsw* h, uint32_t n, uint32_t q, int l, scratch_t* s
     if (locked) pthread_mutex_lock(&h->node_locks[n]);
     uint32_t* r = ROW(h, n, l);
     size_t c = 0;
-    while (c < m && r[c] != ORC_EMPTY) ++c;
-    if (c < m) {
+    int present = 0;
+    for (; c < m && r[c] != ORC_EMPTY; ++c) present = present || r[c] == q;
+    if (present) {
+        /* usearch reconnect_neighbor_nodes_: "If new_slot is already present in
+         * the neighboring connections of close_slot then no need to modify any
+         * connections or run the heuristics" -- a reused slot's kept in-link */
+    } else if (c < m) {
         r[c] = q;
     } else {
         cand_t* C = s->tmp;
@@ -713,10 +729,10 @@ static void insert_slot(orc_hnsw* h, uint32_t q, scratch_t* s, int locked) {
     }
     float dep = orc_distance(h->metric, vq, VEC(h, ep), h->dim);
     s->ndist++;
-    for (int l = maxl; l > L; --l) ep = greedy(h, vq, ep, &dep, l, s, locked);
+    for (int l = maxl; l > L; --l) ep = greedy(h, vq, ep, &dep, l, s, locked, q);
     uint32_t* sel = (uint32_t*)malloc(h->M0 * sizeof(uint32_t));
     for (int l = (L < maxl ? L : maxl); l >= 0; --l) {
-        size_t n = beam(h, vq, ep, dep, h->efC, l, s, locked);
+        size_t n = beam(h, vq, ep, dep, h->efC, l, s, locked, q);
         /* usearch connect_new_node_: refine_(metric, config_.connectivity, ...)
          * on EVERY level -- a new node keeps at most M outgoing links, level 0
          * included; its level-0 row (M0 = 2M slots) fills up to M0 only through
@@ -741,13 +757,29 @@ static void insert_slot(orc_hnsw* h, uint32_t q, scratch_t* s, int locked) {
 
 typedef struct {
     orc_hnsw* h;
-    size_t base;
+    const uint32_t* list; /* slots in insertion order */
     scratch_t* scr;
 } add_ctx;
 
 static void add_one(void* p, size_t i, int tid) {
     add_ctx* c = (add_ctx*)p;
-    insert_slot(c->h, (uint32_t)(c->base + i), &c->scr[tid], 1);
+    insert_slot(c->h, c->list[i], &c->scr[tid], 1);
+}
+
+static void ring_push(orc_hnsw* h, uint32_t slot) {
+    if (h->ring_n == h->ring_cap) {
+        h->ring_cap = h->ring_cap ? 2 * h->ring_cap : 256;
+        h->ring = (uint32_t*)realloc(h->ring, h->ring_cap * sizeof(uint32_t));
+    }
+    h->ring[h->ring_n++] = slot;
+}
+
+/* Clear every row of slot s (levels 0..levels[s]); the level is kept. */
+static void clear_rows(orc_hnsw* h, uint32_t s) {
+    for (int l = 0; l <= h->levels[s]; ++l) {
+        uint32_t* r = ROW(h, s, l);
+        for (size_t i = 0; i < ROWLEN(h, l); ++i) r[i] = ORC_EMPTY;
+    }
 }
 
 int orc_hnsw_add(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n, int threads) {
@@ -771,14 +803,41 @@ int orc_hnsw_add(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n,
         }
         km_free(&tmp);
     }
-    if (h->slots + n > h->cap) {
+    /* free-slot reuse (index_dense_gt::add_ pops free_keys_): the oldest removed
+     * slots first; the entry point's slot is skipped and keeps its place */
+    uint32_t* list = (uint32_t*)malloc(n * sizeof(uint32_t));
+    size_t r = 0;
+    if (h->reuse) {
+        size_t kept = 0;
+        for (size_t i = 0; i < h->ring_n; ++i) {
+            const uint32_t sl = h->ring[i];
+            if (r < n && sl != h->entry) list[r++] = sl;
+            else h->ring[kept++] = sl;
+        }
+        h->ring_n = kept;
+    }
+    const size_t na = n - r;
+    if (h->slots + na > h->cap) {
         size_t want = h->cap ? h->cap : 1024;
-        while (want < h->slots + n) want *= 2;
-        if (orc_hnsw_reserve(h, want)) return 2;
+        while (want < h->slots + na) want *= 2;
+        if (orc_hnsw_reserve(h, want)) {
+            free(list);
+            return 2;
+        }
+    }
+    /* stage the reused slots (index_gt::update): new key and vector, every row
+     * cleared, level kept, live again */
+    for (size_t i = 0; i < r; ++i) {
+        const uint32_t sl = list[i];
+        memcpy(h->vecs + (size_t)sl * h->dim, vecs + i * h->dim, h->dim * sizeof(float));
+        h->keys[sl] = keys[i];
+        h->removed[sl] = 0;
+        km_put(&h->km, keys[i], sl);
+        clear_rows(h, sl);
     }
     size_t base = h->slots;
     size_t need_upper = 0;
-    for (size_t i = 0; i < n; ++i) {
+    for (size_t i = 0; i < na; ++i) {
         uint32_t s = (uint32_t)(base + i);
         int L = orc_sample_level(h->seed, s, (uint32_t)h->M);
         h->levels[s] = (int8_t)L;
@@ -792,39 +851,42 @@ int orc_hnsw_add(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n,
         memset(h->upper + h->upper_cap * h->M, 0xFF, (want - h->upper_cap) * h->M * sizeof(uint32_t));
         h->upper_cap = want;
     }
-    for (size_t i = 0; i < n; ++i) {
+    for (size_t i = 0; i < na; ++i) {
         uint32_t s = (uint32_t)(base + i);
         int L = h->levels[s];
         h->upper_off[s] = L > 0 ? (uint32_t)used : ORC_EMPTY;
         used += (size_t)L;
-        memcpy(h->vecs + (size_t)s * h->dim, vecs + i * h->dim, h->dim * sizeof(float));
-        h->keys[s] = keys[i];
+        memcpy(h->vecs + (size_t)s * h->dim, vecs + (r + i) * h->dim, h->dim * sizeof(float));
+        h->keys[s] = keys[r + i];
         h->removed[s] = 0;
-        km_put(&h->km, keys[i], s);
+        km_put(&h->km, keys[r + i], s);
+        list[r + i] = s;
     }
     atomic_store(&h->upper_used, used);
-    h->slots += n;
+    h->slots += na;
     h->live += n;
 
+    /* insertion order: the reused slots (call order), then the appended ones */
     threads = resolve_threads(threads);
     if ((size_t)threads > n) threads = (int)n;
     if (threads < 1) threads = 1;
     scratch_t* scr = (scratch_t*)malloc(sizeof(scratch_t) * threads);
     for (int t = 0; t < threads; ++t) scratch_init(&scr[t], h->cap, h->efC > h->ef ? h->efC : h->ef, h->M0);
     if (threads == 1) {
-        for (size_t i = 0; i < n; ++i) insert_slot(h, (uint32_t)(base + i), &scr[0], 0);
+        for (size_t i = 0; i < n; ++i) insert_slot(h, list[i], &scr[0], 0);
     } else {
         /* the very first node must exist before concurrent inserts start */
         size_t start = 0;
         if (h->entry == ORC_EMPTY) {
-            insert_slot(h, (uint32_t)base, &scr[0], 0);
+            insert_slot(h, list[0], &scr[0], 0);
             start = 1;
         }
-        add_ctx c = {h, base + start, scr};
+        add_ctx c = {h, list + start, scr};
         parallel_for(n - start, threads, add_one, &c);
     }
     for (int t = 0; t < threads; ++t) scratch_free(&scr[t]);
     free(scr);
+    free(list);
     return 0;
 }
 
@@ -835,11 +897,19 @@ size_t orc_hnsw_remove(orc_hnsw* h, const uint64_t* keys, size_t n) {
         if (km_del(&h->km, keys[i], &s)) {
             h->removed[s] = 1;
             h->live--;
+            ring_push(h, s); /* usearch index_dense_gt::remove: free_keys_.push(slot) */
             ++r;
         }
     }
     return r;
 }
+
+size_t orc_hnsw_free_list(const orc_hnsw* h, uint32_t* out, size_t cap) {
+    for (size_t i = 0; out && i < h->ring_n && i < cap; ++i) out[i] = h->ring[i];
+    return h->ring_n;
+}
+
+void orc_hnsw_set_slot_reuse(orc_hnsw* h, int on) { h->reuse = on ? 1 : 0; }
 
 typedef struct {
     const orc_hnsw* h;
@@ -863,9 +933,10 @@ static void search_one(void* p, size_t qi, int tid) {
         uint32_t ep = h->entry;
         float dep = orc_distance(h->metric, q, VEC(h, ep), h->dim);
         s->ndist++;
-        for (int l = h->max_level; l >= 1; --l) ep = greedy(h, q, ep, &dep, l, s, 0);
+        for (int l = h->max_level; l >= 1; --l) ep = greedy(h, q, ep, &dep, l, s, 0, ORC_EMPTY);
         /* removed entries: traversed, never admitted into the result list */
-        size_t n = h->live < h->slots ? beam_filtered(h, q, ep, dep, c->ef, s) : beam(h, q, ep, dep, c->ef, 0, s, 0);
+        size_t n = h->live < h->slots ? beam_filtered(h, q, ep, dep, c->ef, s)
+                                      : beam(h, q, ep, dep, c->ef, 0, s, 0, ORC_EMPTY);
         for (size_t i = 0; i < n && cnt < c->k; ++i) {
             uint32_t id = s->list[i].id;
             ok[cnt] = h->keys[id];
@@ -942,11 +1013,15 @@ int orc_hnsw_import(orc_hnsw* h, size_t slots, const float* vecs, const uint64_t
     atomic_store(&h->upper_used, n_upper_rows);
     h->slots = slots;
     h->live = 0;
-    for (size_t i = 0; i < slots; ++i)
+    h->ring_n = 0;
+    for (size_t i = 0; i < slots; ++i) {
         if (!removed[i]) {
             km_put(&h->km, keys[i], (uint32_t)i);
             h->live++;
+        } else {
+            ring_push(h, (uint32_t)i); /* no removal order in the interchange: ascending */
         }
+    }
     h->entry = entry;
     h->max_level = max_level;
     return 0;

@@ -82,11 +82,38 @@ void orc_hnsw_params(const orc_hnsw* h, size_t* M, size_t* M0, size_t* efC,
 /* Insert n vectors.  Duplicate live key => returns 3 (usearch: "Duplicate
  * keys not allowed"), nothing inserted.  threads > 1 inserts concurrently
  * (hnswlib-style per-node locks; non-deterministic graph); threads == 1 is
- * the deterministic sequential build. */
+ * the deterministic sequential build.
+ *
+ * Free-slot reuse (usearch index_dense_gt::add_ -> index_gt::update): the
+ * first keys of the call take removed slots from the free ring, oldest
+ * removal first (usearch free_keys_ is a FIFO ring_gt), skipping the slot of
+ * the current entry point; the rest are appended.  A reused slot keeps its
+ * level; at the start of the call it gets its new key and vector, its rows
+ * (every level) are cleared and it is live again; other nodes' links into it
+ * stay.  Then the reused slots are re-linked in call order, then the appended
+ * slots inserted -- each as connect_node_across_levels_ from the entry point.
+ * Rules beyond a plain insert (the usearch v2 series restated):
+ *   - a node is never a candidate of its own insertion (greedy descent and
+ *     beam skip it; usearch asserts "Self-loops are impossible");
+ *   - a reverse link into a row that already holds the node changes nothing
+ *     (reconnect_neighbor_nodes_: "If new_slot is already present in the
+ *     neighboring connections of close_slot then no need to modify any
+ *     connections or run the heuristics");
+ *   - the entry point's own slot is not reused while it is the entry point:
+ *     index_gt::update clears a node's rows before connect_node_across_levels_
+ *     starts from entry_slot_, which would leave the entry point linked only to
+ *     itself (the documented deviation; it stays in the ring, in place). */
 int orc_hnsw_add(orc_hnsw* h, const uint64_t* keys, const float* vecs,
                  size_t n, int threads);
-/* Tombstone keys; returns number removed. */
+/* Tombstone keys; returns number removed.  Each removed slot joins the back of
+ * the free ring (usearch index_dense_gt::remove: free_keys_.push(slot)). */
 size_t orc_hnsw_remove(orc_hnsw* h, const uint64_t* keys, size_t n);
+/* The free ring, oldest first: writes min(count, cap) slots, returns count.
+ * Invariant: the ring holds exactly the removed slots. */
+size_t orc_hnsw_free_list(const orc_hnsw* h, uint32_t* out, size_t cap);
+/* 0 => append-only adds (removed slots stay tombstones; the GPU index's
+ * VSG_FLAG_NO_SLOT_REUSE); 1 (default) => free-slot reuse */
+void orc_hnsw_set_slot_reuse(orc_hnsw* h, int on);
 
 /* k-NN search, ef_override 0 => index expansion_search.  One query per task
  * over `threads` workers (reference granularity, usearch.rs:275-277).
@@ -102,6 +129,8 @@ int orc_hnsw_search(const orc_hnsw* h, const float* queries, size_t nq,
  *   upper[n_upper_rows*M] u32, row (upper_off[s] + l - 1) holds level l. */
 size_t orc_hnsw_upper_rows(const orc_hnsw* h);
 void orc_hnsw_entry(const orc_hnsw* h, uint32_t* entry, int* max_level);
+/* Import takes the removed slots as the free ring in ascending slot order (the
+ * interchange carries no removal order; the GPU index's import does the same). */
 int orc_hnsw_export(const orc_hnsw* h, float* vecs, uint64_t* keys,
                     uint8_t* removed, int8_t* levels, uint32_t* adj0,
                     uint32_t* upper_off, uint32_t* upper);

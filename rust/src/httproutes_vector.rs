@@ -1,5 +1,10 @@
 //! httproutes_vector.rs -- the vector-index HTTP routes over the GPU index actor.
 //!
+//! UNCOMPILED SOURCE: no Rust toolchain exists in this image, and the file is not wired into
+//! a lib.rs here -- tests/test_rust_shim.py checks its routes, fields and statuses against the
+//! Python twin (vsg/httproutes.py) by reading the text.  A maintainer adds
+//! `pub mod httproutes_vector;` beside the reference's httproutes and `cargo check`s it.
+//!
 //! The reference's compiled router (/root/reference/src/httproutes.rs:37-150) serves only
 //! the text backend; its vector routes survive as the client its integration tests call
 //! (/root/reference/tests/integration/httpclient.rs:35-80):
@@ -47,7 +52,7 @@ use axum::response::IntoResponse;
 use axum::response::Response;
 use axum::routing::get;
 use axum::routing::post;
-use scylla::frame::response::result::CqlValue;
+use scylla::value::CqlValue; // as the reference imports it (src/db_index.rs:22, src/index/usearch.rs:317)
 use serde_json::Value;
 use std::collections::HashMap;
 use std::sync::Arc;

@@ -26,6 +26,7 @@ pub const VSG_SCALAR_F16: u32 = 1;
 pub const VSG_NO_KEY: u64 = u64::MAX;
 pub const VSG_FLAG_EXACT_ONLY: u32 = 1;
 pub const VSG_FLAG_F16_TRAVERSAL: u32 = 2;
+pub const VSG_FLAG_NO_SLOT_REUSE: u32 = 4;
 
 #[repr(C)]
 pub struct vsg_index_t {
@@ -72,6 +73,14 @@ pub struct vsg_stats_t {
     pub build_reverse_ns: u64,
     pub build_select_ns: u64,
     pub search_filter_overflow: u64,
+    pub search_filter_reruns: u64,
+    pub slots_reused: u64,
+    pub ktile_copy_failures: u64,
+    pub host_searches: u64,
+    pub host_search_ns: u64,
+    pub host_h2d_ns: u64,
+    pub host_device_ns: u64,
+    pub host_d2h_ns: u64,
 }
 
 /// The native actor's options (src/index/usearch.rs:60-66, 101-118 constants made knobs).
@@ -83,7 +92,7 @@ pub struct vsg_actor_options_t {
     pub reserve_threshold: u64, // 0 => increment / 3
     pub max_batch: u32,         // 0 => 65536 messages per drain
     pub max_wait_us: u32,       // 0 => natural batching
-    pub compact_percent: u32,   // 0 => 50
+    pub compact_percent: u32,   // 0 => never (slots are reused)
     pub concurrent_reads: u32,  // n >= 1 => anns on n read workers beside writes (the reference's fire-and-forget adds)
     pub compact_min_dead: u64,  // 0 => 4096
 }
@@ -107,6 +116,10 @@ pub struct vsg_actor_counters_t {
     pub compactions: u64,
     pub compacted_rows: u64,
     pub compact_errors: u64,
+    pub ann_queue_ns: u64,
+    pub ann_wake_ns: u64,
+    pub batch_search_ns: u64,
+    pub batch_notify_ns: u64,
 }
 
 #[repr(C)]
@@ -156,6 +169,7 @@ extern "C" {
                                 n: usize, stream: *mut c_void) -> c_int;
     // usearch::Index::remove (usearch.rs:215, 245)
     pub fn vsg_index_remove(index: *mut vsg_index_t, keys: *const u64, n: usize, n_removed: *mut usize) -> c_int;
+    pub fn vsg_index_free_slots(index: *const vsg_index_t, out: *mut u32, cap: usize) -> usize;
     // usearch::Index::search (usearch.rs:276), batched; rows padded with VSG_NO_KEY / +inf
     pub fn vsg_index_search(index: *mut vsg_index_t, queries: *const f32, nq: usize, k: usize, ef: usize,
                             out_keys: *mut u64, out_distances: *mut f32, out_counts: *mut usize) -> c_int;

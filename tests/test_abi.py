@@ -41,7 +41,13 @@ def test_version_and_error_strings():
 def test_options_struct_layout_matches_header():
     # vsg_index_options_t: 8 x u32/i32 + u64 = 40 bytes
     assert C.sizeof(_lib.Options) == 40
-    assert C.sizeof(_lib.Stats) == 17 * 8  # vsg_stats_t: 17 x u64 (search_filter_overflow since round 4)
+    # vsg_stats_t: the header's uint64_t fields, in order, are the ctypes mirror's
+    import re
+    txt = open(_lib.HEADER).read()
+    body = txt[:txt.index("} vsg_stats_t;")].rsplit("typedef struct {", 1)[1]
+    fields = re.findall(r"uint64_t\s+(\w+);", body)
+    assert [f for f, _ in _lib.Stats._fields_] == fields
+    assert C.sizeof(_lib.Stats) == len(fields) * 8
 
 
 def test_invalid_options_rejected_without_device():

@@ -163,14 +163,50 @@ def test_actor_capacity_growth_rule():
     a.close()
 
 
-def test_actor_upsert_stream_compacts():
-    """A CDC-style upsert stream (every write a replace) leaves a tombstone per
-    replace; the actor compacts once they reach compact_percent, and answers
-    stay those of the live rows."""
+def test_actor_upsert_stream_reuses_slots():
+    """A CDC-style upsert stream (every write a replace = remove + add,
+    usearch.rs:214-221) under free-slot reuse: each replace's freed slot is
+    re-linked by the next add, so the index does not grow and never needs a
+    compaction; answers are those of the live rows."""
+    dim, nkeys = 32, 3000
+    rng = np.random.default_rng(9)
+    a = Actor(dim, "l2sq", connectivity=16, expansion_add=64, expansion_search=64, seed=2)
+    cur = {}
+    for rnd in range(4):
+        vals = rng.integers(0, 32, (nkeys, dim)).astype(np.float32)
+        for k in range(nkeys):
+            a.add_or_replace(k, vals[k])
+            cur[k] = vals[k]
+    a.flush()
+    c = a.counters()
+    assert c["compactions"] == 0 and c["add_errors"] == 0, c
+    assert a.count() == nkeys
+    h = lib().vsg_actor_index(a._h)
+    s = C.c_size_t()
+    check(lib().vsg_index_graph_info(h, C.byref(s), None, None, None, None))
+    assert s.value <= nkeys + 1  # the entry point's slot may wait in the ring
+    q = rng.integers(0, 32, (40, dim)).astype(np.float32)
+    keys = np.empty((40, 10), np.uint64)
+    dist = np.empty((40, 10), np.float32)
+    check(lib().vsg_index_exact_search(h, C.c_void_p(q.ctypes.data), 40, 10, C.c_void_p(keys.ctypes.data),
+                                       C.c_void_p(dist.ctypes.data), None))
+    mat = np.stack([cur[k] for k in range(nkeys)])
+    _, od, _ = O.exact_search("l2sq", mat, q, 10)
+    np.testing.assert_array_equal(dist, od)
+    for k in range(0, nkeys, 97):  # each key answers with its latest vector
+        kk, dd = a.ann(cur[k], 1)
+        assert dd[0] == 0.0
+    a.close()
+
+
+def test_actor_upsert_stream_compacts_append_only():
+    """The same stream on an append-only index (VSG_FLAG_NO_SLOT_REUSE) leaves a
+    tombstone per replace; the actor compacts once they reach compact_percent, and
+    answers stay those of the live rows."""
     dim, nkeys = 32, 3000
     rng = np.random.default_rng(9)
     a = Actor(dim, "l2sq", connectivity=16, expansion_add=64, expansion_search=64, seed=2,
-              compact_percent=40, compact_min_dead=1000)
+              compact_percent=40, compact_min_dead=1000, slot_reuse=False)
     cur = {}
     for rnd in range(4):
         vals = rng.integers(0, 32, (nkeys, dim)).astype(np.float32)

@@ -10,8 +10,9 @@ the 16-chunk f16 kernel instances comparable with the oracle (f32 rows) bit for 
   (a) oracle-built 20k-row graph (with tombstones) imported into an f16 index: GPU search
       == oracle search, keys and distances, at ef 64 / 192 / 1024 (the register kernel's
       R classes up to its largest);
-  (b) GPU-built 200k-row graph: recall@10 >= the oracle's own sequential build - 0.5 % at
-      ef 64 and 192, same ground truth;
+  (b) GPU-built 200k-row graph: recall@10 within +-0.5 % of the oracle's own build at
+      ef 64 and 192, same ground truth (two-sided: a GPU graph much better than the
+      restatement's would be a divergence too);
   (c) one full C4 shard, 12.5M x 128 f16 built on the GPU: recall@10 >= 0.95 at ef 192 on
       10,000 queries against the GPU exact search, and that exact search checked against
       numpy on 1,000 queries -- bit for bit, since the distances are exact integers and
@@ -81,7 +82,7 @@ def test_c4_gpu_build_recall_vs_oracle_build():
             rc = recall(orc.search(q, K, ef, threads=_cores())[0], gt.keys)
             rg = recall(gpu.search(q, K, ef).keys, gt.keys)
             print(f"C4 200k ef={ef}: GPU build {rg:.4f}, oracle build {rc:.4f}")
-            assert rg >= rc - 0.005, (ef, rg, rc)
+            assert abs(rg - rc) <= 0.005, (ef, rg, rc)
     finally:
         O.set_fast_metric(False)
 

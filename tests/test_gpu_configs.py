@@ -139,3 +139,100 @@ def test_c5_1m1536_ip_mfma_vs_valu_full_size(nq, monkeypatch):
     if xh is not None:  # the MFMA tile of B=64 against the oracle at full size
         ok, od, _ = O.exact_search("ip", xh, q.cpu().numpy(), k, threads=16)
         assert_topk_matches_oracle(mk[:, :k], md[:, :k], ok, od)
+
+
+@pytest.mark.timeout(1200)
+def test_c4_100m128_f16_eight_row_shards_merged():
+    """C4 as configured (configs[3]): 100M x 128 SIFT-like integer rows, f16 HBM
+    storage, l2sq, as 8 row shards of 12.5M built one after another on this GPU (the
+    8-GPU run is the driver's), every query searched on every shard, per-shard top-k
+    merged by the HIP merge kernel.  The rows are integers in 0..255: every f16
+    element and every squared-L2 sum is exact, so the merged exact top-k equals the
+    oracle's brute force over all 100M rows (run shard by shard, merged by (distance,
+    key)) bit for bit on 1,000 queries; merged HNSW recall@10 >= 0.95 at the per-shard
+    ef the 8-shard emulation needs (160, profiles/r04_configs_c4.jsonl) on 10,000
+    queries against the merged exact ground truth."""
+    import torch
+    n, dim, shards, nq, nq_o, k = 100_000_000, 128, 8, 10_000, 1000, 10
+    bs, qs, ms = G.config_seeds(3)
+    q = vsg.datagen_device("sift", nq, dim, qs, ms)
+    qh = q[:nq_o].cpu().numpy()
+    parts, ork, ord_ = [], [], []
+    O.set_fast_metric(True)  # exact on integer data in any summation order
+    try:
+        for s in range(shards):
+            lo, hi = s * n // shards, (s + 1) * n // shards
+            x = vsg.datagen_device("sift", hi - lo, dim, bs, ms, start=lo)
+            idx = vsg.Index(dim, "l2sq", "f16", 16, 128, 64, seed=0x5EED + s)
+            idx.reserve(hi - lo)
+            keys = np.arange(lo, hi, dtype=np.uint64)
+            idx.add_device(keys, x)
+            torch.cuda.synchronize()
+            xh = x.cpu().numpy()
+            del x
+            assert np.all(xh[:4096] == np.rint(xh[:4096])) and xh.max() <= 255
+            sk, sd, _ = O.exact_search("l2sq", xh, qh, k, keys=keys, threads=16)
+            del xh
+            ork.append(sk)
+            ord_.append(sd)
+            parts.append(idx)
+    finally:
+        O.set_fast_metric(False)
+    assert sum(p.size() for p in parts) == n
+
+    def merged(ef, exact=False):
+        outs = [p.search_device(q, k, ef, exact=exact) for p in parts]
+        mk, md = vsg.merge_topk_device(torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs]), k)
+        return mk.cpu().numpy().view(np.uint64), md.cpu().numpy()
+
+    ek, ed = merged(0, exact=True)
+    ak, ad = np.concatenate(ork, axis=1), np.concatenate(ord_, axis=1)
+    o = np.lexsort((ak, ad), axis=1)[:, :k]
+    np.testing.assert_array_equal(ek[:nq_o], np.take_along_axis(ak, o, 1))
+    np.testing.assert_array_equal(ed[:nq_o], np.take_along_axis(ad, o, 1))
+    r = {ef: recall(merged(ef)[0], ek, k) for ef in (128, 160, 192)}
+    print("C4 8-shard merged recall@10 by per-shard ef:", r)
+    assert r[160] >= 0.95 and r[192] >= r[160] - 0.002
+
+
+@pytest.mark.timeout(900)
+def test_c5_1m1536_ip_hnsw_leg():
+    """C5's HNSW half (configs[4] "brute-force MFMA path vs HNSW"): 1M x 1536 f32 IP
+    HNSW (M=16, efC=128) built on the GPU reaches recall@10 >= 0.95 against the f32
+    MFMA exact ground truth (the probe's operating point, ef 30: 0.952,
+    profiles/r04_configs_c5.jsonl); and at 200k rows the GPU build's recall is within
+    +-0.5 % of the oracle's own build at matched ef (the north-star bar, two-sided)."""
+    import torch
+    dim, k, nq = 1536, 10, 5000
+    bs, qs, ms = G.config_seeds(4)
+    q = vsg.datagen_device("clustered", nq, dim, qs, ms)
+    n = 1_000_000
+    x = vsg.datagen_device("clustered", n, dim, bs, ms)
+    idx = vsg.Index(dim, "ip", "f32", 16, 128, 64, seed=0x5EED)
+    idx.reserve(n)
+    idx.add_device(np.arange(n, dtype=np.uint64), x)
+    gt = idx.search_device(q, k, exact=True)[0]
+    torch.cuda.synchronize()
+    gt = gt.cpu().numpy().view(np.uint64)
+    r = {ef: recall(idx.search_device(q, k, ef)[0].cpu().numpy().view(np.uint64), gt, k) for ef in (24, 32, 48, 64)}
+    print("C5 1M x 1536 IP HNSW recall@10 by ef:", r)
+    assert r[48] >= 0.95 and r[64] >= r[32] >= r[24] - 0.002
+    # 200k rows: GPU build vs the oracle build (threaded, host-ISA metrics), same ground truth
+    m = 200_000
+    xh = x[:m].cpu().numpy()
+    del x, idx
+    small = vsg.Index(dim, "ip", "f32", 16, 128, 64, seed=0x5EED)
+    small.add(np.arange(m, dtype=np.uint64), xh)
+    qh = q[:2000].cpu().numpy()
+    gt2 = small.exact_search(qh, k).keys
+    O.set_fast_metric(True)
+    try:
+        orc = O.HnswOracle(dim, "ip", 16, 128, 64, seed=0x5EED)
+        orc.add(np.arange(m, dtype=np.uint64), xh, threads=16)
+        for ef in (24, 64):
+            rc = recall(orc.search(qh, k, ef, threads=16)[0], gt2, k)
+            rg = recall(small.search(qh, k, ef).keys, gt2, k)
+            print(f"C5 200k ef={ef}: GPU build {rg:.4f}, oracle build {rc:.4f}")
+            assert abs(rg - rc) <= 0.005, (ef, rg, rc)
+    finally:
+        O.set_fast_metric(False)

@@ -270,3 +270,90 @@ def test_oracle_matches_literal_usearch_loops(frac):
             lk, ld = lit.search(q[i], 6, ef)
             assert k[i][: int(c[i])].tolist() == lk, (ef, i)
             np.testing.assert_array_equal(d[i][: int(c[i])], np.array(ld, np.float32))
+
+
+def _graph_rows(g, s, l):
+    row = g["adj0"][s] if l == 0 else g["upper"][int(g["upper_off"][s]) + l - 1]
+    return row[row != 0xFFFFFFFF].tolist()
+
+
+@pytest.mark.parametrize("metric", ["l2sq", "ip"])
+def test_oracle_slot_reuse_matches_literal_usearch_update(metric):
+    """Free-slot reuse (usearch index_dense add_ -> index_gt::update, the
+    reference's replace = remove + add, /root/reference/src/index/usearch.rs:
+    214-221, 245): remove/add churn in calls of 1 and of several keys, the C
+    restatement against the literal transcription -- same free ring, same slot
+    for every key, identical graph (every row, order included) and identical
+    search results with the tombstones left over."""
+    import usearch_literal as UL
+    n, dim, M, efc = 300, 12, 6, 24
+    x = G.clustered(n + 400, dim, 31, 8)
+    if metric == "ip":
+        x = x / np.linalg.norm(x, axis=1, keepdims=True)
+    q = G.clustered(30, dim, 33, 8)
+    h = O.HnswOracle(dim, metric, M, efc, 16, seed=23)
+    lit = UL.LiteralHnsw(dim, metric, M, efc, seed=23)
+    h.add(np.arange(n), x[:n], threads=1)
+    for i in range(n):
+        lit.add(i, x[i])
+    slot_key = {i: i for i in range(n)}
+    rng = np.random.default_rng(7)
+    nxt = n
+    for step in range(12):
+        live = [s for s in slot_key if s not in lit.removed]
+        rm = rng.choice(live, int(rng.integers(1, 25)), replace=False)
+        h.remove(np.array([slot_key[int(s)] for s in rm], np.uint64))
+        lit.remove(rm)
+        np.testing.assert_array_equal(h.free_list(), np.array(list(lit.free), np.uint32))
+        nadd = int(rng.integers(1, 30)) if step % 3 else 1
+        keys = np.arange(nxt, nxt + nadd, dtype=np.uint64)
+        vecs = x[nxt:nxt + nadd]  # fresh rows: no exact ties (the literal compares distances only)
+        h.add(keys, vecs, threads=1)
+        slots = lit.add_batch(list(vecs))
+        for key, s in zip(keys, slots):
+            slot_key[s] = int(key)
+        nxt += nadd
+        np.testing.assert_array_equal(h.free_list(), np.array(list(lit.free), np.uint32))
+    g = h.export()
+    assert (g["entry"], g["max_level"]) == (lit.entry, lit.max_level)
+    assert len(g["keys"]) == len(lit.vecs)
+    for s in range(len(lit.vecs)):
+        assert int(g["keys"][s]) == slot_key[s] or s in lit.removed
+        assert bool(g["removed"][s]) == (s in lit.removed)
+        for l in range(int(g["levels"][s]) + 1):
+            assert _graph_rows(g, s, l) == lit.links[s][l], (s, l)
+    for ef in (6, 16, 50):
+        k, d, c = h.search(q, 6, ef)
+        for i in range(len(q)):
+            ls, ld = lit.search(q[i], 6, ef)
+            assert k[i][: int(c[i])].tolist() == [slot_key[s] for s in ls], (ef, i)
+            np.testing.assert_array_equal(d[i][: int(c[i])], np.array(ld, np.float32))
+
+
+def test_oracle_slot_reuse_rules():
+    """The reuse rules on their own: a replaced key takes the OLDEST free slot
+    (FIFO), keeps that slot's level, never links to itself, the entry point's
+    slot stays in the ring while it is the entry, rows hold no duplicate ids,
+    and with reuse off the add appends (round-4 behaviour)."""
+    n, dim = 2000, 16
+    x = G.clustered(n + 200, dim, 41, 8)
+    h = O.HnswOracle(dim, "l2sq", 8, 48, 32, seed=3)
+    h.add(np.arange(n), x[:n], threads=1)
+    g0 = h.export()
+    e, _ = h.entry()
+    rm = np.array([17, int(e), 5, 900], np.uint64)  # slot == key here
+    h.remove(rm)
+    assert h.free_list().tolist() == [17, e, 5, 900]
+    h.add(np.array([n, n + 1], np.uint64), x[n:n + 2], threads=1)
+    g = h.export()
+    assert h.free_list().tolist() == [e, 900]        # 17 then 5 reused; the entry skipped
+    assert int(g["keys"][17]) == n and int(g["keys"][5]) == n + 1
+    assert g["levels"][17] == g0["levels"][17] and g["levels"][5] == g0["levels"][5]
+    assert h.slots() == n and h.size() == n - 2
+    for s in range(h.slots()):
+        for l in range(int(g["levels"][s]) + 1):
+            row = _graph_rows(g, s, l)
+            assert s not in row and len(set(row)) == len(row), (s, l)
+    h.set_slot_reuse(False)
+    h.add(np.array([n + 2], np.uint64), x[n + 2:n + 3], threads=1)
+    assert h.slots() == n + 1 and h.free_list().tolist() == [e, 900]

@@ -18,7 +18,15 @@ break / admission conditions:
                              keep c unless dist(c, kept) < c.distance
   connect_new_node_          refine_(connectivity) on every level
   reconnect_neighbor_nodes_  append below connectivity_max (level ? M : M0),
-                             else refine_(connectivity_max) over the row + new
+                             else refine_(connectivity_max) over the row + new;
+                             a row already holding the new node is left as is
+  index_dense add_ / update  removed slots queue in free_keys_ (a FIFO ring);
+                             an add pops the oldest and re-links it in place
+                             (index_gt::update: rows cleared, level kept,
+                             other nodes' links into it kept), else appends.
+                             The node is never its own candidate; the entry
+                             point's slot is not reused while it is the entry
+                             (see oracle/vsg_oracle.h orc_hnsw_add)
 
 Distances come from the oracle's f32 metric (oracle.distance), so on float data
 without exact ties the set formulation (oracle/vsg_oracle.c beam(),
@@ -29,6 +37,7 @@ Pure Python: small graphs only.
 from __future__ import annotations
 
 import heapq
+from collections import deque
 
 import numpy as np
 
@@ -43,19 +52,22 @@ class LiteralHnsw:
         self.levels: list[int] = []
         self.links: list[list[list[int]]] = []  # links[slot][level] = ordered neighbours
         self.removed: set[int] = set()
+        self.free: deque[int] = deque()  # index_dense free_keys_, oldest removal first
         self.entry, self.max_level = 0xFFFFFFFF, -1
 
     def _d(self, a, b) -> float:
         return O.distance(self.metric, a, b)
 
     # search_for_one_: greedy on levels begin_level .. end_level + 1
-    def _search_for_one(self, q, closest, begin, end):
+    def _search_for_one(self, q, closest, begin, end, exclude=None):
         cd = self._d(q, self.vecs[closest])
         for level in range(begin, end, -1):
             changed = True
             while changed:
                 changed = False
                 for c in self.links[closest][level]:
+                    if c == exclude:     # never its own candidate
+                        continue
                     d = self._d(q, self.vecs[c])
                     if d < cd:
                         cd, closest, changed = d, c, True
@@ -66,7 +78,7 @@ class LiteralHnsw:
         r = self._d(q, self.vecs[start])
         nxt = [(r, start)]               # min-heap
         top = [(-r, start)]              # max-heap via negation
-        visited = {start}
+        visited = {start, new}           # `new` is never its own candidate
         while nxt:
             cd, cs = nxt[0]
             if cd > -top[0][0] and len(top) == top_limit:
@@ -100,15 +112,47 @@ class LiteralHnsw:
 
     def add(self, slot, vec):
         assert slot == len(self.vecs)
-        vec = np.ascontiguousarray(vec, np.float32)
+        self._append(vec)
+        self._connect(slot)
+
+    def _append(self, vec):
+        slot = len(self.vecs)
         L = O.sample_level(self.seed, slot, self.M)
-        self.vecs.append(vec)
+        self.vecs.append(np.ascontiguousarray(vec, np.float32))
         self.levels.append(L)
         self.links.append([[] for _ in range(L + 1)])
+        return slot
+
+    def add_batch(self, vecs):
+        """One add call of several vectors, as orc_hnsw_add stages it: free slots
+        (oldest removal first, the entry point's skipped) take the first vectors
+        -- new vector, rows cleared, level kept, live again -- the rest are
+        appended; then the reused slots are re-linked in order, then the
+        appended ones.  Returns the slots in call order."""
+        picks, rest = [], deque()
+        while self.free and len(picks) < len(vecs):
+            s = self.free.popleft()
+            (picks if s != self.entry else rest).append(s)
+        self.free = rest + self.free
+        slots = []
+        for s, v in zip(picks, vecs):
+            self.vecs[s] = np.ascontiguousarray(v, np.float32)
+            self.links[s] = [[] for _ in range(self.levels[s] + 1)]
+            self.removed.discard(s)
+            slots.append(s)
+        for v in vecs[len(picks):]:
+            slots.append(self._append(v))
+        for s in slots:
+            self._connect(s)
+        return slots
+
+    # connect_node_across_levels_ (index_gt::add / update)
+    def _connect(self, slot):
+        vec, L = self.vecs[slot], self.levels[slot]
         if self.entry == 0xFFFFFFFF:
             self.entry, self.max_level = slot, L
             return
-        closest = self._search_for_one(vec, self.entry, self.max_level, L)
+        closest = self._search_for_one(vec, self.entry, self.max_level, L, exclude=slot)
         for level in range(min(L, self.max_level), -1, -1):
             top = self._search_to_insert(vec, closest, slot, level, self.efc)
             self.links[slot][level] = self._refine(top, self.M)          # connect_new_node_
@@ -116,6 +160,8 @@ class LiteralHnsw:
             cmax = self.M if level else self.M0                          # reconnect_neighbor_nodes_
             for c in self.links[slot][level]:
                 row = self.links[c][level]
+                if slot in row:                  # already present: nothing changes
+                    continue
                 if len(row) < cmax:
                     row.append(slot)
                     continue
@@ -126,7 +172,11 @@ class LiteralHnsw:
             self.entry, self.max_level = slot, L
 
     def remove(self, slots):
-        self.removed.update(int(s) for s in slots)
+        for s in slots:
+            s = int(s)
+            if s not in self.removed:
+                self.removed.add(s)
+                self.free.append(s)      # index_dense_gt::remove: free_keys_.push(slot)
 
     # index_dense search: search_for_one_ to level 0, then search_to_find_in_base_
     def search(self, q, k, ef):

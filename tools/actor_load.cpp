@@ -87,6 +87,8 @@ int main(int argc, char** argv) {
 
     vsg_actor_counters_t c0{};
     vsg_actor_counters(a, &c0);
+    vsg_stats_t s0{};
+    vsg_index_stats(h, &s0);
     std::vector<double> lat(nq);
     std::vector<uint64_t> ak(nq * k);
     std::atomic<int> mismatch{0}, errors{0};
@@ -120,6 +122,8 @@ int main(int argc, char** argv) {
     const double served_s = std::chrono::duration<double>(clk::now() - t0).count();
     vsg_actor_counters_t c1{};
     vsg_actor_counters(a, &c1);
+    vsg_stats_t s1{};
+    vsg_index_stats(h, &s1);
     // diagnostics: does the batched answer itself drift after the load?
     {
         std::vector<uint64_t> bk2(nq * k);
@@ -149,6 +153,23 @@ int main(int argc, char** argv) {
     }
     std::sort(lat.begin(), lat.end());
     const uint64_t calls = c1.search_calls - c0.search_calls;
+    double lat_mean = 0;
+    for (double x : lat) lat_mean += x;
+    lat_mean /= (double)nq;
+    // where an ann's time goes (us): per ann, queueing before its batch starts and the
+    // wake-up after its completion; per batch, the search call (host staging + H2D +
+    // kernels + D2H + sync; VSG_PROFILE_HOST_SEARCH=1 splits the device part) and the
+    // copies + completion signals of its anns
+    const double na = (double)(c1.anns - c0.anns), nb = (double)std::max<uint64_t>(1, calls);
+    const double hs = (double)std::max<uint64_t>(1, s1.host_searches - s0.host_searches);
+    std::fprintf(stderr,
+                 "{\"breakdown_us\": {\"ann_latency_mean\": %.1f, \"ann_queue_mean\": %.1f, \"ann_wake_mean\": %.1f, "
+                 "\"batch_search_mean\": %.1f, \"batch_notify_mean\": %.1f, \"host_search_wall_mean\": %.1f, "
+                 "\"h2d_mean\": %.1f, \"device_mean\": %.1f, \"d2h_mean\": %.1f}}\n",
+                 lat_mean, (c1.ann_queue_ns - c0.ann_queue_ns) / 1e3 / na, (c1.ann_wake_ns - c0.ann_wake_ns) / 1e3 / na,
+                 (c1.batch_search_ns - c0.batch_search_ns) / 1e3 / nb, (c1.batch_notify_ns - c0.batch_notify_ns) / 1e3 / nb,
+                 (s1.host_search_ns - s0.host_search_ns) / 1e3 / hs, (s1.host_h2d_ns - s0.host_h2d_ns) / 1e3 / hs,
+                 (s1.host_device_ns - s0.host_device_ns) / 1e3 / hs, (s1.host_d2h_ns - s0.host_d2h_ns) / 1e3 / hs);
     std::printf(
         "{\"rows\": %zu, \"dim\": %zu, \"clients\": %d, \"queries\": %zu, \"k\": %zu, \"ef\": %zu, "
         "\"max_wait_us\": %u, \"read_workers\": %u, \"actor_qps\": %.1f, \"batched_qps\": %.1f, \"lat_us_p50\": %.1f, "

@@ -21,6 +21,21 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def provenance():
+    """Which kernels were profiled: bench.kernel_src_sha() of this tree (bench.py uses
+    the summary only while its tree hashes the same) and the git head when known."""
+    from bench import kernel_src_sha
+    head = None
+    try:
+        import subprocess
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip() or None
+    except Exception:  # noqa: BLE001 -- the GPU box's copy has no .git
+        pass
+    return {"kernel_src_sha": kernel_src_sha(), "git_head": head}
 
 
 def per_dispatch(d, counter, kernel):
@@ -59,6 +74,7 @@ def search(fdir, wdir, n, dim, nq, ef, metric, path=None):
         "write_size_kib_raw": round(write_kib, 1),
         "hbm_bytes_per_launch": int(2 * fetch_kib * 1024 + write_kib * 1024),
         "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes",
+        **provenance(),
     }
     json.dump(out, open(path or os.path.join(ROOT, "profiles", "search_pmc.json"), "w"), indent=1)
     return out
@@ -68,7 +84,8 @@ def build(fdir, wdir, n, dim, metric, M, efc, path=None):
     out = {"workload": {"n": int(n), "dim": int(dim), "metric": metric, "M": int(M), "efc": int(efc),
                         "forward_links": "M"},
            "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes; summed over every "
-                         "dispatch of the kernel in ONE build (the probe builds once per process)"}
+                         "dispatch of the kernel in ONE build (the probe builds once per process)",
+           **provenance()}
     # "hnsw_insert_": the fused insert kernel or both launches of the split insert
     # (hnsw_insert_beam_kernel + hnsw_insert_select_kernel), then each on its own
     for tag, kern in (("insert", "hnsw_insert_"), ("beam", "hnsw_insert_beam_kernel"),

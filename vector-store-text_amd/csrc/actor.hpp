@@ -25,6 +25,7 @@
 // search returns the first k live entries of its list).
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -69,9 +70,11 @@ struct ActorConfig {
     size_t max_batch = 65536;            // messages drained per worker wake-up
     uint32_t max_wait_us = 0;            // optional coalescing window (0: natural batching)
     // compact once tombstones reach this percentage of the stored rows (and at
-    // least compact_min_dead rows); >= 100 disables.  Replaces keep the old row
-    // as a tombstone (usearch.rs:214-221), so an upsert stream needs this.
-    uint32_t compact_percent = 50;
+    // least compact_min_dead rows); >= 100 disables (the default since round 5:
+    // a replace's remove frees its slot and the next add re-links it in place,
+    // usearch index_dense's free-slot reuse, so an upsert stream no longer grows
+    // the index; compaction only returns the slots of net deletes)
+    uint32_t compact_percent = 100;
     size_t compact_min_dead = 4096;
     // Anns on their own workers, beside the writes (needs a backend whose search
     // may run concurrently with add/remove, as vsg_index's does): 0 = submission
@@ -87,7 +90,17 @@ struct ActorCounters {
     uint64_t add_errors = 0, remove_errors = 0, search_errors = 0;
     uint64_t max_search_batch = 0, max_add_batch = 0;
     uint64_t compactions = 0, compacted_rows = 0, compact_errors = 0;
+    // serving-path time breakdown (steady clock, ns), summed: per ann, enqueue ->
+    // its batch starts and the waiter's wake-up (finish -> caller running); per
+    // search batch, the batched search call and the result copies + wake calls
+    uint64_t ann_queue_ns = 0, ann_wake_ns = 0, batch_search_ns = 0, batch_notify_ns = 0;
 };
+
+inline uint64_t steady_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 class Actor {
   public:
@@ -103,10 +116,12 @@ class Actor {
         float* dist = nullptr;
         size_t count = 0;  // Ann: results written; Count: live size
         std::string err;   // backend message when rc != 0
+        uint64_t t_fin = 0;  // steady_ns() at finish (wake-up latency)
         void finish(int r) {
             std::lock_guard<std::mutex> lk(m);
             rc = r;
             done = true;
+            t_fin = steady_ns();
             cv.notify_all();
         }
         int wait() {
@@ -124,6 +139,7 @@ class Actor {
         Kind kind;
         uint64_t key = 0;
         size_t k = 0;
+        uint64_t t_enq = 0;  // steady_ns() at submission
         std::vector<float> vec;
         Waiter* w = nullptr;
         AddDone done = nullptr;
@@ -187,6 +203,7 @@ class Actor {
         m.w = &w;
         push(std::move(m));
         const int rc = w.wait();
+        wake_ns_.fetch_add(steady_ns() - w.t_fin, std::memory_order_relaxed);
         if (count) *count = w.count;
         if (err) *err = w.err;
         return rc;
@@ -220,11 +237,14 @@ class Actor {
 
     ActorCounters counters() const {
         std::lock_guard<std::mutex> lk(cm_);
-        return ctr_;
+        ActorCounters c = ctr_;
+        c.ann_wake_ns = wake_ns_.load(std::memory_order_relaxed);
+        return c;
     }
 
   private:
     void push(Msg&& m) {
+        m.t_enq = steady_ns();
         const bool read = cfg_.concurrent_reads > 0 && m.kind == ANN;
         {
             std::lock_guard<std::mutex> lk(qm_);
@@ -376,9 +396,13 @@ class Actor {
     void anns(std::vector<Msg>& b, size_t i0, size_t i1) {
         const size_t d = be_->dimensions();
         const size_t ef0 = be_->expansion_search();
+        const uint64_t t0 = steady_ns();
         {
+            uint64_t qw = 0;
+            for (size_t i = i0; i < i1; ++i) qw += t0 - std::min(t0, b[i].t_enq);
             std::lock_guard<std::mutex> lk(cm_);
             ctr_.anns += i1 - i0;
+            ctr_.ann_queue_ns += qw;
         }
         // group by effective ef so batching cannot change any result
         std::unordered_map<size_t, std::vector<size_t>> groups;
@@ -406,12 +430,15 @@ class Actor {
             keys.resize(g.size() * kmax);
             dist.resize(g.size() * kmax);
             counts.resize(g.size());
+            const uint64_t ts = steady_ns();
             const int rc = be_->search(qs.data(), g.size(), kmax, e, keys.data(), dist.data(), counts.data());
+            const uint64_t tn = steady_ns();
             {
                 std::lock_guard<std::mutex> lk(cm_);
                 ctr_.search_calls++;
                 ctr_.max_search_batch = std::max<uint64_t>(ctr_.max_search_batch, g.size());
                 if (rc) ctr_.search_errors += g.size();
+                ctr_.batch_search_ns += tn - ts;
             }
             for (size_t r = 0; r < g.size(); ++r) {
                 Msg& m = b[g[r]];
@@ -429,6 +456,9 @@ class Actor {
                 }
                 m.w->finish(rc);
             }
+            const uint64_t dn = steady_ns() - tn;
+            std::lock_guard<std::mutex> lk(cm_);
+            ctr_.batch_notify_ns += dn;
         }
     }
 
@@ -440,6 +470,7 @@ class Actor {
     bool stop_ = false;
     mutable std::mutex cm_;
     ActorCounters ctr_;
+    std::atomic<uint64_t> wake_ns_{0};  // ann wake-up latency, summed (lock-free: every caller adds)
     std::thread worker_;
     std::vector<std::thread> readers_;
 };

@@ -46,9 +46,10 @@ size_t insert_lds_bytes(int efc, int hash, int m0) { return wave_lds_bytes(hash,
 // candidate starts there (merge() reports the lowest position it filled).
 // (Prefetching the next entry's adjacency row during this expansion's distance
 // loads measured 2-7% slower: profiles/r01_search_phases.jsonl.)
+// self: the node an insert (re)links, never admitted (VSG_EMPTY in searches).
 template <int G, int VM, int U, typename T, int MET>
 __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t ep, float dep,
-                           WaveLds& w, uint64_t& ndist, uint64_t& nadj, BeamProf& pf) {
+                           WaveLds& w, uint64_t& ndist, uint64_t& nadj, BeamProf& pf, uint32_t self = VSG_EMPTY) {
     const int lane = lane_id();
     const int m = l == 0 ? g.M0 : g.M;
     w.vis.clear();
@@ -78,7 +79,7 @@ __device__ void beam_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, ui
             const uint32_t nb = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
             const bool full = __ballot(nb != VSG_EMPTY) == ~0ull;
             bool fresh = false, evicted = false;
-            if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
+            if (nb != VSG_EMPTY && nb != self) fresh = w.vis.insert(nb, evicted);
             const uint64_t mask = __ballot(fresh);
             lossy = lossy || __ballot(evicted) != 0;
             const int cnt = popc64(mask);
@@ -494,17 +495,17 @@ __global__ __launch_bounds__(64) void hnsw_insert_kernel(InsertParams p) {
     uint32_t cur = p.entry;
     float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
     ++ndist;
-    for (int l = p.max_level; l > L; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+    for (int l = p.max_level; l > L; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, node);
     uint32_t pos = p.pair_off[bi];
     for (int l = min(L, p.max_level); l >= 0; --l) {
         if (p.efc <= 192) {
             // candidate set in VGPRs (hnsw_regset.hpp), then the sorted top-efc
             // list the selection walks -- the list beam's exact result
             RegSet<VSG_BUILD_REG_R> B;
-            beam_reg<G, VM, U, T, MET, VSG_BUILD_REG_R>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf);
+            beam_reg<G, VM, U, T, MET, VSG_BUILD_REG_R>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf, node);
             regset_to_list<VSG_BUILD_REG_R>(B, p.efc, w);
         } else {
-            beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, pf);
+            beam_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, pf, node);
         }
         // usearch connect_new_node_: at most M forward links on every level
         // (refine_ with config_.connectivity); level-0 rows reach M0 = 2M only
@@ -575,10 +576,10 @@ __global__ __launch_bounds__(64) void hnsw_insert_beam_kernel(InsertParams p) {
     uint32_t cur = p.entry;
     float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
     ++ndist;
-    for (int l = p.max_level; l > L; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+    for (int l = p.max_level; l > L; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj, node);
     for (int l = min(L, p.max_level); l >= 0; --l) {
         RegSet<VSG_BUILD_REG_R> B;
-        beam_reg<G, VM, U, T, MET, VSG_BUILD_REG_R>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf);
+        beam_reg<G, VM, U, T, MET, VSG_BUILD_REG_R>(g, q, l, cur, dcur, p.efc, w, B, ndist, nadj, pf, node);
         regset_to_list<VSG_BUILD_REG_R>(B, p.efc, w);
         const size_t slot = (size_t)p.list_off[bi] + (size_t)l;
         const int n = w.list.size;
@@ -647,6 +648,19 @@ __global__ __launch_bounds__(64) VSG_SEL_WAVES void hnsw_insert_select_kernel(In
 // Pairs sorted by (level, v, u).  Persistent waves scan contiguous chunks for
 // segment heads; each segment (level, v) is merged into v's row: append while
 // there is room, else heuristic re-selection over existing + incoming.
+// Re-linking reused slots (p.flags set: bit 1 marks the call's reused slots),
+// an incoming u that v's row already holds -- a link into the slot kept from
+// before its removal -- changes nothing (usearch reconnect_neighbor_nodes_,
+// oracle add_reverse); only those segments take the checks.
+
+#define VSG_FLAG_RELINK 2  // d_flags bit 1: a reused slot being re-linked by the current add
+
+// does row[0, ne) hold u (one lane; the row was just read, so from L1/L2)
+__device__ __forceinline__ bool row_holds(const uint32_t* row, int ne, uint32_t u) {
+    bool h = false;
+    for (int c = 0; c < ne; ++c) h = h || row[c] == u;
+    return h;
+}
 
 // Entries in use of an adjacency row (a compact prefix), read by one lane: 16 B
 // at a time when rows are 16-B aligned (m % 4 == 0), stopping at the first piece
@@ -733,7 +747,11 @@ __global__ __launch_bounds__(64) VSG_REV_WAVES void hnsw_reverse_kernel(ReverseP
                 const int m = l == 0 ? g.M0 : g.M;
                 uint32_t* row = g.row(v, l);
                 const int ne = row_fill(row, m);
-                if (ne + nin <= m) {
+                bool relink = false;  // a reused slot among the incoming: the wave-wide path checks it
+                if (p.flags)
+                    for (int t = 0; t < nin; ++t)
+                        relink = relink || (p.flags[(uint32_t)(p.keys[i + t] & PAIR_ID_MASK)] & VSG_FLAG_RELINK);
+                if (!relink && ne + nin <= m) {
                     fits = true;
                     float* rowd = g.adjd0 ? g.rowd(v, l) : nullptr;
                     for (int t = 0; t < nin; ++t) {
@@ -777,10 +795,47 @@ __global__ __launch_bounds__(64) VSG_REV_WAVES void hnsw_reverse_kernel(ReverseP
                 if (xm != ~0ull) break;
             }
             float* rowd = g.adjd0 ? g.rowd(v, l) : nullptr;
-            if (ne + nin <= m) {
-                for (int t = lane; t < nin; t += 64) {
-                    row[ne + t] = (uint32_t)(p.keys[h + t] & PAIR_ID_MASK);
-                    if (rowd) rowd[ne + t] = __uint_as_float(p.vals[h + t]);
+            // re-linked reused slots: incoming links v's row already holds are dropped
+            bool anyrel = false;
+            if (p.flags)
+                for (int t = 0; t < nin; t += 64) {
+                    const bool valid = t + lane < nin;
+                    const uint32_t u = valid ? (uint32_t)(p.keys[h + t + lane] & PAIR_ID_MASK) : 0u;
+                    anyrel = anyrel || __ballot(valid && (p.flags[u] & VSG_FLAG_RELINK)) != 0;
+                }
+            auto kept_in = [&](int idx) {  // incoming idx (< nin) survives the check
+                if (!anyrel) return true;
+                const uint32_t u = (uint32_t)(p.keys[h + idx] & PAIR_ID_MASK);
+                return !((p.flags[u] & VSG_FLAG_RELINK) && row_holds(row, ne, u));
+            };
+            int nkeep = nin;
+            if (anyrel) {
+                nkeep = 0;
+                for (int t = 0; t < nin; t += 64) nkeep += popc64(__ballot(t + lane < nin && kept_in(t + lane)));
+                if (nkeep == 0) {
+                    ++nappend;
+                    continue;
+                }
+            }
+            if (ne + nkeep <= m) {
+                if (!anyrel) {
+                    for (int t = lane; t < nin; t += 64) {
+                        row[ne + t] = (uint32_t)(p.keys[h + t] & PAIR_ID_MASK);
+                        if (rowd) rowd[ne + t] = __uint_as_float(p.vals[h + t]);
+                    }
+                } else {
+                    int at = ne;
+                    for (int t = 0; t < nin; t += 64) {
+                        const bool keep = t + lane < nin && kept_in(t + lane);
+                        const uint64_t km = __ballot(keep);
+                        wave_sync();  // every lane's row_holds read precedes this chunk's writes
+                        if (keep) {
+                            const int pos = at + lanes_below(km);
+                            row[pos] = (uint32_t)(p.keys[h + t + lane] & PAIR_ID_MASK);
+                            if (rowd) rowd[pos] = __uint_as_float(p.vals[h + t + lane]);
+                        }
+                        at += popc64(km);
+                    }
                 }
                 ++nappend;
                 continue;
@@ -819,7 +874,7 @@ __global__ __launch_bounds__(64) VSG_REV_WAVES void hnsw_reverse_kernel(ReverseP
                 }
             }
             for (int t = 0; t < nin; t += 64) {
-                const bool valid = t + lane < nin;
+                const bool valid = t + lane < nin && kept_in(t + lane);
                 const size_t idx = h + t + lane;
                 const float cd = valid ? __uint_as_float(p.vals[idx]) : 0.f;
                 const uint32_t ci = valid ? (uint32_t)(p.keys[idx] & PAIR_ID_MASK) : 0u;
@@ -875,6 +930,116 @@ __global__ __launch_bounds__(64) void edge_dist_fill_kernel(DevGraph gd, const i
             if (xm != ~0ull) break;
         }
     }
+}
+
+// ----------------------------------------------------------- slot reuse --
+// An add that reuses removed slots (usearch index_dense_gt::add_ popping
+// free_keys_ -> index_gt::update; oracle orc_hnsw_add) stages them before its
+// first batch: prepared row, |x|^2 and key into the slot, every row of the
+// slot cleared (its level and upper rows are kept), flags = removed | relink
+// until the add publishes (searches keep treating it as removed; the reverse
+// kernel sees the relink bit).  One wave per reused slot.
+__global__ __launch_bounds__(64) void reuse_stage_kernel(DevGraph g, uint8_t* __restrict__ vecs,
+                                                         float* __restrict__ sqnorm, uint64_t* __restrict__ okeys,
+                                                         uint8_t* __restrict__ flags, const uint8_t* __restrict__ rows,
+                                                         const float* __restrict__ sq, const uint64_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ slots,
+                                                         const int8_t* __restrict__ levels, uint32_t n) {
+    const int lane = lane_id();
+    const size_t n16 = g.row_bytes / 16;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t s = slots[i];
+        const uint4* a = reinterpret_cast<const uint4*>(rows + (size_t)i * g.row_bytes);
+        uint4* b = reinterpret_cast<uint4*>(vecs + (size_t)s * g.row_bytes);
+        for (size_t c = lane; c < n16; c += 64) b[c] = a[c];
+        if (lane == 0) {
+            if (sqnorm) sqnorm[s] = sq[i];
+            okeys[s] = keys[i];
+            flags[s] = 1 | VSG_FLAG_RELINK;
+        }
+        for (int l = 0; l <= levels[i]; ++l) {
+            const int m = l == 0 ? g.M0 : g.M;
+            uint32_t* row = l == 0 ? g.adj0 + (size_t)s * g.M0 : g.upper + ((size_t)g.upper_off[s] + (size_t)(l - 1)) * g.M;
+            for (int j = lane; j < m; j += 64) row[j] = VSG_EMPTY;
+            if (g.adjd0) {
+                float* rd = l == 0 ? g.adjd0 + (size_t)s * g.M0 : g.upperd + ((size_t)g.upper_off[s] + (size_t)(l - 1)) * g.M;
+                for (int j = lane; j < m; j += 64) rd[j] = __builtin_inff();
+            }
+        }
+    }
+}
+
+hipError_t launch_reuse_stage(const DevGraph& g, uint8_t* vecs, float* sqnorm, uint64_t* keys_out, uint8_t* flags,
+                              const uint8_t* rows, const float* sq, const uint64_t* keys, const uint32_t* slots,
+                              const int8_t* levels, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>(n, 1u << 20);
+    hipLaunchKernelGGL(reuse_stage_kernel, dim3(grid), dim3(64), 0, s, g, vecs, sqnorm, keys_out, flags, rows, sq,
+                       keys, slots, levels, (uint32_t)n);
+    return hipGetLastError();
+}
+
+// The stored distance of every link INTO a reused slot (kept from before its
+// removal) was computed against the slot's old vector: recompute it against the
+// new one, dist(v, slot) with v as the query -- the value an insert stores
+// (operand-symmetric, same lane order), so the reverse prune reads exactly the
+// distances the oracle recomputes.  One wave per slot v (grid-stride); only
+// rows that hold a relink-flagged id load v's vector.
+template <int G, int VM, int U, typename T, int MET>
+__global__ __launch_bounds__(64) void edge_dist_refresh_kernel(DevGraph gd, const int8_t* levels, const uint8_t* flags,
+                                                               uint32_t n) {
+    __shared__ uint32_t todo[64];
+    __shared__ float tdist[64];
+    __shared__ int pos[64];
+    const int lane = lane_id();
+    const GraphDev g = to_dev(gd);
+    for (uint32_t s = blockIdx.x; s < n; s += gridDim.x) {
+        if (flags[s] & VSG_FLAG_RELINK) continue;  // a reused slot itself: its rows were cleared
+        QReg<G, VM, T> q;
+        bool loaded = false;
+        for (int l = 0; l <= levels[s]; ++l) {
+            const int m = l == 0 ? g.M0 : g.M;
+            const uint32_t* row = g.row(s, l);
+            float* rd = g.rowd(s, l);
+            for (int c0 = 0; c0 < m; c0 += 64) {
+                const uint32_t x = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
+                const uint64_t xm = __ballot(x != VSG_EMPTY);
+                const bool hit = x != VSG_EMPTY && (flags[x] & VSG_FLAG_RELINK);
+                const uint64_t hm = __ballot(hit);
+                if (hm) {
+                    if (!loaded) {
+                        q.load(g.vec(s), g.nchunks);
+                        loaded = true;
+                    }
+                    const int cnt = popc64(hm);
+                    if (hit) {
+                        todo[lanes_below(hm)] = x;
+                        pos[lanes_below(hm)] = c0 + lane;
+                    }
+                    wave_sync();
+                    rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, todo, cnt, q, tdist);
+                    wave_sync();
+                    if (lane < cnt) rd[pos[lane]] = tdist[lane];
+                    wave_sync();
+                }
+                if (xm != ~0ull) break;
+            }
+        }
+    }
+}
+
+hipError_t launch_edge_dist_refresh(Storage st, MetricKind mk, const DevGraph& g, const int8_t* levels,
+                                    const uint8_t* flags, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (!g.adjd0) return hipErrorInvalidValue;
+    hipError_t err = hipSuccess;
+    const unsigned grid = (unsigned)std::min<size_t>(n, 1u << 20);
+    dispatch_all(st, mk, g.nchunks, [&](auto sh, auto tt, auto mt) {
+        auto kern = VSG_KERNEL_OF(edge_dist_refresh_kernel, sh, tt, mt);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, s, g, levels, flags, (uint32_t)n);
+        err = hipGetLastError();
+    });
+    return err;
 }
 
 hipError_t launch_edge_dist_fill(Storage st, MetricKind mk, const DevGraph& g, const int8_t* levels, size_t n,

@@ -93,9 +93,12 @@ __device__ inline float dist_one(const GraphDev& g, const QReg<G, VM, T>& q, uin
 // neighbour (lexicographic (distance, slot)) until none improves.  Rows longer
 // than a wave (M0 = 2M > 64, M <= 64) are read in 64-entry pieces; rows are a
 // compact prefix, so a piece that ends in EMPTY ends the row (oracle read_row).
+// self: the node being (re)linked by an insert, never its own candidate (a
+// reused slot is reachable through other nodes' kept links; oracle greedy());
+// VSG_EMPTY in searches.
 template <int G, int VM, int U, typename T, int MET>
 __device__ void greedy_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t& cur,
-                             float& dcur, WaveLds& w, uint64_t& ndist, uint64_t& nadj) {
+                             float& dcur, WaveLds& w, uint64_t& ndist, uint64_t& nadj, uint32_t self = VSG_EMPTY) {
     const int lane = lane_id();
     const int m = l == 0 ? g.M0 : g.M;
     for (;;) {
@@ -105,23 +108,26 @@ __device__ void greedy_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, 
         ++nadj;
         for (int c0 = 0; c0 < m; c0 += 64) {
             const uint32_t nb = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
-            const bool ok = nb != VSG_EMPTY;
+            const uint64_t pm = __ballot(nb != VSG_EMPTY);  // the row's entries in this piece
+            const bool ok = nb != VSG_EMPTY && nb != self;
             const uint64_t mask = __ballot(ok);
             const int cnt = popc64(mask);
             if (ok) w.todo[lanes_below(mask)] = nb;
             wave_sync();
-            if (cnt == 0) break;
-            rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
-            wave_sync();
-            ndist += (uint64_t)cnt;
-            const float cd = lane < cnt ? w.tdist[lane] : __builtin_inff();
-            const uint32_t ci = lane < cnt ? w.todo[lane] : VSG_EMPTY;
-            if (cand_less(cd, ci, d, id)) {
-                d = cd;
-                id = ci;
+            if (pm == 0) break;
+            if (cnt) {
+                rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
+                wave_sync();
+                ndist += (uint64_t)cnt;
+                const float cd = lane < cnt ? w.tdist[lane] : __builtin_inff();
+                const uint32_t ci = lane < cnt ? w.todo[lane] : VSG_EMPTY;
+                if (cand_less(cd, ci, d, id)) {
+                    d = cd;
+                    id = ci;
+                }
+                wave_sync();
             }
-            wave_sync();
-            if (cnt < 64) break;
+            if (pm != ~0ull) break;  // compact prefix: the row ended inside this piece
         }
         wave_argmin(d, id);
         if (id != VSG_EMPTY && cand_less(d, id, dcur, cur)) {

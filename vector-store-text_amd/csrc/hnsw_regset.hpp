@@ -277,9 +277,10 @@ __device__ __forceinline__ void admit(RegSet<R>& B, bool mine, uint64_t ck, bool
 // slower: the runner-up is rarely still next (profiles/r01_search_phases.jsonl).
 // Prefetching only the runner-up's adjacency row: C4 shard search -8 %, C2
 // search +2 %, C2 build -5 % (profiles/r02_search_probes.jsonl) -- not kept.
+// self: the node an insert (re)links, never admitted (VSG_EMPTY in searches).
 template <int G, int VM, int U, typename T, int MET, int R>
 __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t ep, float dep, int ef, WaveLds& w,
-                         RegSet<R>& B, uint64_t& ndist, uint64_t& nadj, BeamProf& pf) {
+                         RegSet<R>& B, uint64_t& ndist, uint64_t& nadj, BeamProf& pf, uint32_t self = VSG_EMPTY) {
     const int lane = lane_id();
     // select on values (readfirstlane), not on field addresses: a
     // select-of-loads folded into a load-of-select pinned the graph
@@ -337,7 +338,7 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
             const uint32_t nb = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
             const bool full = __ballot(nb != VSG_EMPTY) == ~0ull;
             bool fresh = false, evicted = false;
-            if (nb != VSG_EMPTY) fresh = w.vis.insert(nb, evicted);
+            if (nb != VSG_EMPTY && nb != self) fresh = w.vis.insert(nb, evicted);
             const uint64_t mask = __ballot(fresh);
             lossy = lossy || __ballot(evicted) != 0;
             const int cnt = popc64(mask);
@@ -513,10 +514,12 @@ __device__ __forceinline__ void admit_filt(RegSet<R>& B, FiltState& F, bool mine
 // removed.  ep == VSG_EMPTY: B already holds a seed set (opt-in multi-entry
 // descent); its removed flags are read here and the radius while no seed is
 // live is the largest seed key.
+// stop: end the traversal at the first overflow (the caller re-runs the query
+// on a list that cannot overflow) instead of degrading.
 template <int G, int VM, int U, typename T, int MET, int R>
 __device__ __forceinline__ void beam_reg_filt(const GraphDev& g, const QReg<G, VM, T>& q, const uint8_t* flags,
                                               uint32_t ep, float dep, int ef, WaveLds& w, RegSet<R>& B, FiltState& F,
-                                              uint64_t& ndist, uint64_t& nadj, BeamProf& pf) {
+                                              uint64_t& ndist, uint64_t& nadj, BeamProf& pf, bool stop = false) {
     const int lane = lane_id();
     const int m0r = __builtin_amdgcn_readfirstlane(g.M0);
     const uint32_t* adj0 = g.adj0;
@@ -605,8 +608,9 @@ __device__ __forceinline__ void beam_reg_filt(const GraphDev& g, const QReg<G, V
                 admit_filt<R>(B, F, lane < cnt, ck, crm, lossy, ef, sk, sf);
                 pf.merge += VSG_CLK() - t2;
             }
-            if (!full) break;
+            if (!full || (stop && F.degraded)) break;
         }
+        if (stop && F.degraded) break;
     }
 }
 

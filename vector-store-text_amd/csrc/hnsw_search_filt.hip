@@ -17,10 +17,15 @@
 //   hnsw_search_filt_kernel      -- sorted LDS list holding live and removed
 //       entries (VSG_REM_BIT), cut at the ef-th live entry; ef up to MAX_EF or
 //       when the register set would be too small.
-// Both count entries they had to drop for want of room in stats[16]
-// (vsg_stats_t.search_filter_overflow, 0 at the sizes the index's removed
-// fraction selects in every test): exactness holds while that counter stays 0;
-// past it a query degrades to the live-only traversal (hnsw_regset.hpp
+// A query whose candidate set runs out of room (a high removed fraction at
+// large ef: the removed nodes at or below the radius pile up beside the ef
+// live ones) stops, is flagged (p.ovf) and counted in stats[16]
+// (vsg_stats_t.search_filter_overflow), and
+//   hnsw_search_filt_rerun_kernel -- the same sorted-list beam on a list in
+//       device memory sized for every slot (it holds distinct nodes only, so
+//       it cannot run out of room) -- searches it again, counted in stats[17].
+// No query ever returns a degraded answer; without p.ovf
+// (probes) a query degrades to the live-only traversal (hnsw_regset.hpp
 // FiltState), which always terminates.
 #include <hip/hip_runtime.h>
 
@@ -37,12 +42,16 @@ __device__ __forceinline__ int xcd_query(const SearchParams& p) {
     return x * qd + min(x, rm) + j;
 }
 
-__device__ __forceinline__ void filt_stats(const SearchParams& p, uint64_t ndist, uint64_t nadj, uint32_t overflow) {
-    if (lane_id() == 0 && p.stats) {
-        atomicAdd(&p.stats[0], (unsigned long long)ndist);
-        atomicAdd(&p.stats[1], (unsigned long long)nadj);
-        atomicAdd(&p.stats[2], 1ull);
-        if (overflow) atomicAdd(&p.stats[16], (unsigned long long)overflow);
+__device__ __forceinline__ void filt_stats(const SearchParams& p, uint64_t ndist, uint64_t nadj, uint32_t overflow,
+                                           int qi) {
+    if (lane_id() == 0) {
+        if (p.ovf) p.ovf[qi] = overflow ? 1 : 0;
+        if (p.stats) {
+            atomicAdd(&p.stats[0], (unsigned long long)ndist);
+            atomicAdd(&p.stats[1], (unsigned long long)nadj);
+            atomicAdd(&p.stats[2], 1ull);
+            if (overflow) atomicAdd(&p.stats[16], p.ovf ? 1ull : (unsigned long long)overflow);
+        }
     }
 }
 
@@ -72,11 +81,13 @@ __global__ __launch_bounds__(64) void hnsw_search_reg_filt_kernel(SearchParams p
             // (removed nodes included) seeds the filtered level-0 beam
             for (int l = p.max_level; l >= 2; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
             beam_reg<G, VM, U, T, MET, R>(g, q, 1, cur, dcur, min(p.upper_ef, p.ef), w, B, ndist, nadj, pf);
-            beam_reg_filt<G, VM, U, T, MET, R>(g, q, p.flags, VSG_EMPTY, 0.f, p.ef, w, B, F, ndist, nadj, pf);
+            beam_reg_filt<G, VM, U, T, MET, R>(g, q, p.flags, VSG_EMPTY, 0.f, p.ef, w, B, F, ndist, nadj, pf,
+                                               p.ovf != nullptr);
         } else {
             // usearch search_for_one_: the upper levels ignore the predicate
             for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
-            beam_reg_filt<G, VM, U, T, MET, R>(g, q, p.flags, cur, dcur, p.ef, w, B, F, ndist, nadj, pf);
+            beam_reg_filt<G, VM, U, T, MET, R>(g, q, p.flags, cur, dcur, p.ef, w, B, F, ndist, nadj, pf,
+                                               p.ovf != nullptr);
         }
         overflow = F.overflow;
         // results: the live keys in ascending order (the first k of `top`)
@@ -107,7 +118,7 @@ __global__ __launch_bounds__(64) void hnsw_search_reg_filt_kernel(SearchParams p
         od[j] = __builtin_inff();
     }
     if (lane == 0 && p.out_counts) p.out_counts[qi] = (uint32_t)count;
-    filt_stats(p, ndist, nadj, overflow);
+    filt_stats(p, ndist, nadj, overflow, qi);
 }
 
 // The filtered beam on a sorted LDS list of capacity w.list.cap >= ef + 64:
@@ -115,9 +126,12 @@ __global__ __launch_bounds__(64) void hnsw_search_reg_filt_kernel(SearchParams p
 // live entries are in, the list is cut right after the ef-th (the radius), so
 // every entry is at or below it; before that the radius is the last live entry
 // (the start's key while there is none).
+// (The list may live in device memory instead: hnsw_search_filt_rerun_kernel.)
+// stop: end the traversal at the first overflow instead of degrading.
 template <int G, int VM, int U, typename T, int MET>
 __device__ void beam_level_filt(const GraphDev& g, const QReg<G, VM, T>& q, const uint8_t* flags, uint32_t ep,
-                                float dep, int ef, WaveLds& w, uint64_t& ndist, uint64_t& nadj, uint32_t& overflow) {
+                                float dep, int ef, WaveLds& w, uint64_t& ndist, uint64_t& nadj, uint32_t& overflow,
+                                bool stop = false) {
     const int lane = lane_id();
     const int m = g.M0;
     w.vis.clear();
@@ -202,6 +216,10 @@ __device__ void beam_level_filt(const GraphDev& g, const QReg<G, VM, T>& q, cons
                 } else {
                     nlive = nl;
                     lastlive = last;
+                    if (lost && stop) {
+                        overflow += (uint32_t)lost;  // re-run by the caller
+                        return;
+                    }
                     if (lost) {
                         // Out of room before ef live entries: degrade (counted).  Every
                         // removed entry leaves the list and removed candidates are
@@ -260,7 +278,7 @@ __global__ __launch_bounds__(64) void hnsw_search_filt_kernel(SearchParams p, in
         float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
         ++ndist;
         for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
-        beam_level_filt<G, VM, U, T, MET>(g, q, p.flags, cur, dcur, p.ef, w, ndist, nadj, overflow);
+        beam_level_filt<G, VM, U, T, MET>(g, q, p.flags, cur, dcur, p.ef, w, ndist, nadj, overflow, p.ovf != nullptr);
         const List& L = w.list;
         for (int r = 0; r < L.size && count < p.k; r += 64) {
             const int i = r + lane;
@@ -283,7 +301,108 @@ __global__ __launch_bounds__(64) void hnsw_search_filt_kernel(SearchParams p, in
         od[j] = __builtin_inff();
     }
     if (lane == 0 && p.out_counts) p.out_counts[qi] = (uint32_t)count;
-    filt_stats(p, ndist, nadj, overflow);
+    filt_stats(p, ndist, nadj, overflow, qi);
+}
+
+// Re-run of the queries that overflowed (p.ovf[qi] set): persistent blocks, one
+// wave each, walk the flags; block b's list (d0 | d1 | i0 | i1, cap entries each)
+// is list b of p.filt_lists in device memory, cap >= every slot + 64 (the list
+// holds distinct nodes: forgotten ids are de-duplicated against it), so it never
+// runs out of room.  The visited table stays in LDS.  Same beam, same results as
+// the LDS-list kernel would give with room enough: the oracle's beam_filtered().
+template <int G, int VM, int U, typename T, int MET>
+__global__ __launch_bounds__(64) void hnsw_search_filt_rerun_kernel(SearchParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = lane_id();
+    const GraphDev g = to_dev(p.g);
+    const size_t cap = (size_t)p.filt_cap;
+    uint8_t* mine = p.filt_lists + (size_t)blockIdx.x * cap * 16;
+    for (int qi = blockIdx.x; qi < p.nq; qi += gridDim.x) {
+        if (!p.ovf[qi]) continue;  // wave-uniform
+        WaveLds w = carve(smem, 0, p.hash_size, 0);
+        w.list.d0 = reinterpret_cast<float*>(mine);
+        w.list.d1 = reinterpret_cast<float*>(mine + cap * 4);
+        w.list.i0 = reinterpret_cast<uint32_t*>(mine + cap * 8);
+        w.list.i1 = reinterpret_cast<uint32_t*>(mine + cap * 12);
+        w.list.cap = (int)cap;
+        uint64_t ndist = 0, nadj = 0;
+        uint32_t overflow = 0;
+        int count = 0;
+        uint64_t* ok = p.out_keys + (size_t)qi * p.k;
+        float* od = p.out_dist + (size_t)qi * p.k;
+        QReg<G, VM, T> q;
+        q.load(p.queries + (size_t)qi * g.row_bytes, g.nchunks);
+        uint32_t cur = p.entry;
+        float dcur = dist_one<G, VM, U, T, MET>(g, q, cur, w);
+        ++ndist;
+        for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+        beam_level_filt<G, VM, U, T, MET>(g, q, p.flags, cur, dcur, p.ef, w, ndist, nadj, overflow);
+        const List& L = w.list;
+        for (int r = 0; r < L.size && count < p.k; r += 64) {
+            const int i = r + lane;
+            const bool valid = i < L.size;
+            const uint32_t e = valid ? L.I()[i] : VSG_REM_BIT;
+            const bool alive = !(e & VSG_REM_BIT);
+            const uint32_t id = e & VSG_ID_MASK;
+            const uint64_t mk = __ballot(alive);
+            const int pos = count + lanes_below(mk);
+            if (alive && pos < p.k) {
+                ok[pos] = p.keys ? p.keys[id] : (uint64_t)id;
+                od[pos] = L.D()[i];
+            }
+            count += popc64(mk);
+        }
+        if (count > p.k) count = p.k;
+        for (int j = count + lane; j < p.k; j += 64) {
+            ok[j] = ~0ull;
+            od[j] = __builtin_inff();
+        }
+        if (lane == 0) {
+            if (p.out_counts) p.out_counts[qi] = (uint32_t)count;
+            if (p.stats) {
+                atomicAdd(&p.stats[0], (unsigned long long)ndist);
+                atomicAdd(&p.stats[1], (unsigned long long)nadj);
+                atomicAdd(&p.stats[17], 1ull);
+                if (overflow) atomicAdd(&p.stats[16], (unsigned long long)overflow);  // cannot happen (cap)
+            }
+        }
+        wave_sync();
+    }
+}
+
+// One list per re-run block: 16 B x (slots + 64) entries; as many lists as fit
+// in 256 MiB (at least one, at most 16).
+void filt_rerun_shape(size_t slots, int* cap, int* nlists) {
+    const size_t c = slots + 64;
+    const size_t per = c * 16;
+    size_t nl = ((size_t)256 << 20) / per;
+    nl = nl < 1 ? 1 : nl > 16 ? 16 : nl;
+    *cap = (int)c;
+    *nlists = (int)nl;
+}
+size_t filt_rerun_bytes(size_t slots) {
+    int cap = 0, nl = 0;
+    filt_rerun_shape(slots, &cap, &nl);
+    return (size_t)cap * 16 * (size_t)nl;
+}
+
+static hipError_t launch_filt_rerun(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s) {
+    if (!p.ovf || !p.filt_lists || p.filt_nlists < 1) return hipSuccess;
+    SearchParams r = p;
+    // the visited table only (the list is in device memory): forgetful at this size
+    r.hash_size = std::max(1024, std::min(p.hash_size, 16384));
+    const size_t lds = search_reg_lds_bytes(r.hash_size);
+    hipError_t err = hipSuccess;
+    dispatch_all<true>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+        constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
+        using T = typename decltype(tt)::T;
+        constexpr int MET = decltype(mt)::MET;
+        auto kern = hnsw_search_filt_rerun_kernel<G, VM, U, T, MET>;
+        if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3((unsigned)std::min(p.filt_nlists, p.nq)), dim3(64), lds, s, r);
+        err = hipGetLastError();
+    });
+    return err;
 }
 
 // Candidate-set size of a filtered search: the ef live keys, the removed ones
@@ -325,6 +444,7 @@ hipError_t launch_search_filt(Storage st, MetricKind mk, const SearchParams& p, 
                     c.out_keys = p.out_keys + (size_t)off * p.k;
                     c.out_dist = p.out_dist + (size_t)off * p.k;
                     c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
+                    c.ovf = p.ovf ? p.ovf + off : nullptr;
                     hipLaunchKernelGGL(kern, dim3(c.nq), dim3(64), lds, s, c);
                     err = hipGetLastError();
                 }
@@ -336,6 +456,7 @@ hipError_t launch_search_filt(Storage st, MetricKind mk, const SearchParams& p, 
         };
         if (rows == 17) dispatch_all<false>(st, mk, p.g.nchunks, body);
         else dispatch_all<true>(st, mk, p.g.nchunks, body);
+        if (err == hipSuccess) err = launch_filt_rerun(st, mk, p, s);
         return err;
     }
     // sorted LDS list: 16 B per entry, up to 8,192 entries (ef <= MAX_EF live ones and
@@ -361,10 +482,12 @@ hipError_t launch_search_filt(Storage st, MetricKind mk, const SearchParams& p, 
             c.out_keys = p.out_keys + (size_t)off * p.k;
             c.out_dist = p.out_dist + (size_t)off * p.k;
             c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
+            c.ovf = p.ovf ? p.ovf + off : nullptr;
             hipLaunchKernelGGL(kern, dim3(c.nq), dim3(64), lds, s, c, cap);
             err = hipGetLastError();
         }
     });
+    if (err == hipSuccess) err = launch_filt_rerun(st, mk, p, s);
     return err;
 }
 

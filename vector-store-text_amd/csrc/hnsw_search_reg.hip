@@ -28,6 +28,10 @@
 // dozen VALU instructions instead of dependent LDS searches.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "hnsw_common.hpp"
 #include "hnsw_regset.hpp"
 #include "vsg_dispatch.hpp"
@@ -39,14 +43,7 @@ namespace vsg {
 #define VSG_SEARCH_ATTR
 #endif
 template <int G, int VM, int U, typename T, int MET, int R>
-__global__ __launch_bounds__(64) VSG_SEARCH_ATTR void hnsw_search_reg_kernel(SearchParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    int qi = blockIdx.x;
-    if (p.xcd_map) {
-        const int nq = p.nq, qd = nq >> 3, rm = nq & 7;
-        const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-        qi = x * qd + min(x, rm) + j;
-    }
+__device__ __forceinline__ void search_reg_one(const SearchParams& p, int qi, uint8_t* smem) {
     const int lane = lane_id();
     const GraphDev g = to_dev(p.g);
     WaveLds w = carve(smem, 0, p.hash_size, 0);
@@ -131,10 +128,53 @@ __global__ __launch_bounds__(64) VSG_SEARCH_ATTR void hnsw_search_reg_kernel(Sea
     }
 }
 
+template <int G, int VM, int U, typename T, int MET, int R>
+__global__ __launch_bounds__(64) VSG_SEARCH_ATTR void hnsw_search_reg_kernel(SearchParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (p.qnext) {
+        // persistent grid (VSG_SEARCH_PERSIST, probes): resident waves take query
+        // indices from a counter until the batch is done
+        for (;;) {
+            int qi = 0;
+            if (lane_id() == 0) qi = (int)atomicAdd(p.qnext, 1u);
+            qi = __builtin_amdgcn_readfirstlane(qi);
+            if (qi >= p.nq) break;
+            search_reg_one<G, VM, U, T, MET, R>(p, qi, smem);
+            wave_sync();
+        }
+        return;
+    }
+    int qi = blockIdx.x;
+    if (p.xcd_map) {
+        const int nq = p.nq, qd = nq >> 3, rm = nq & 7;
+        const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+        qi = x * qd + min(x, rm) + j;
+    }
+    search_reg_one<G, VM, U, T, MET, R>(p, qi, smem);
+}
+
 // slots per lane: 64 R >= ef + 64 (a compaction leaves room for a full batch)
 static inline int reg_rows(int ef) { return ef <= 64 ? 2 : ef <= 192 ? 4 : ef <= 448 ? 8 : 17; }
 
 size_t search_reg_lds_bytes(int hash) { return wave_lds_bytes(hash, 0, 0); }
+
+// one-wave workgroups of `kern` resident on the whole device at `lds` bytes each
+// (occupancy x CUs), cached per (device, kernel, lds)
+static int resident_blocks(const void* kern, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, const void*, size_t>, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({dev, kern, lds});
+    if (it != cache.end()) return it->second;
+    int cus = 0, per_cu = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds);
+    const int r = std::max(1, per_cu * cus);
+    cache[{dev, kern, lds}] = r;
+    return r;
+}
 
 hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s) {
     if (p.nq <= 0) return hipSuccess;
@@ -163,7 +203,13 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
                 c.out_keys = p.out_keys + (size_t)off * p.k;
                 c.out_dist = p.out_dist + (size_t)off * p.k;
                 c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
-                hipLaunchKernelGGL(kern, dim3(c.nq), dim3(64), lds, s, c);
+                unsigned grid = (unsigned)c.nq;
+                if (p.qnext) {  // persistent: one round of resident waves, counter reset per launch
+                    grid = (unsigned)std::max(1, std::min(c.nq, resident_blocks((const void*)kern, lds)));
+                    err = hipMemsetAsync(p.qnext, 0, sizeof(unsigned), s);
+                    if (err != hipSuccess) break;
+                }
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, c);
                 err = hipGetLastError();
             }
         };

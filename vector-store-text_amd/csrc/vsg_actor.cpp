@@ -82,7 +82,7 @@ vsg::ActorConfig actor_config(const vsg_actor_options_t* o) {
     cfg.reserve_threshold = o->reserve_threshold ? o->reserve_threshold : cfg.reserve_increment / 3;
     if (o->max_batch) cfg.max_batch = o->max_batch;
     cfg.max_wait_us = o->max_wait_us;
-    if (o->compact_percent) cfg.compact_percent = o->compact_percent;
+    if (o->compact_percent) cfg.compact_percent = o->compact_percent;  // 0 => never (vsg.h)
     if (o->compact_min_dead) cfg.compact_min_dead = o->compact_min_dead;
     cfg.concurrent_reads = o->concurrent_reads;  // 0, 1, or n read workers (capped at 8)
     return cfg;
@@ -235,6 +235,10 @@ int vsg_actor_counters(const vsg_actor_t* a, vsg_actor_counters_t* out) {
     out->compactions = c.compactions;
     out->compacted_rows = c.compacted_rows;
     out->compact_errors = c.compact_errors;
+    out->ann_queue_ns = c.ann_queue_ns;
+    out->ann_wake_ns = c.ann_wake_ns;
+    out->batch_search_ns = c.batch_search_ns;
+    out->batch_notify_ns = c.batch_notify_ns;
     return VSG_OK;
 }
 

@@ -45,6 +45,18 @@ struct SearchParams {
     // hnsw_search_filt.hip).  removed_frac sizes the candidate set.
     int filt;
     float removed_frac;
+    // Filtered searches only.  ovf[qi] = 1: query qi's candidate set ran out of
+    // room (registers / LDS list) and the query stopped; launch_search_filt then
+    // searches it again on a sorted list in device memory (filt_lists, filt_cap
+    // entries per list, filt_nlists lists) that holds every slot, so no result is
+    // ever a degraded one.  ovf == nullptr: no re-run (degrades, counted).
+    uint8_t* ovf;
+    uint8_t* filt_lists;
+    int filt_cap, filt_nlists;
+    // register kernel, probes (VSG_SEARCH_PERSIST=1): a persistent grid of resident
+    // waves pulling query indices from this counter (zeroed per launch); nullptr:
+    // one workgroup per query
+    unsigned* qnext;
 };
 
 struct InsertParams {
@@ -79,6 +91,10 @@ struct ReverseParams {
     const uint32_t* vals;  // f32 bits: dist(u, v)
     size_t npairs;
     unsigned long long* stats;
+    // re-link pass of an add that reuses removed slots: the index flags, bit 1 =
+    // a reused slot of this add (incoming links a row already holds are
+    // dropped); nullptr otherwise (no check)
+    const uint8_t* flags;
 };
 
 struct ExactParams {
@@ -175,8 +191,12 @@ size_t insert_lds_bytes(int efc, int hash, int m0);
 
 hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
 hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
-// filtered search (p.filt): register set when it fits, else the sorted LDS list
+// filtered search (p.filt): register set when it fits, else the sorted LDS list;
+// overflowed queries re-run on device-memory lists (p.ovf, p.filt_lists)
 hipError_t launch_search_filt(Storage st, MetricKind mk, const SearchParams& p, hipStream_t s);
+// device-memory list scratch of the re-run: bytes for `slots`, and the list count / capacity it holds
+size_t filt_rerun_bytes(size_t slots);
+void filt_rerun_shape(size_t slots, int* cap, int* nlists);
 size_t search_reg_lds_bytes(int hash);
 // split insert: beam kernel then selection kernel (efc <= 192: register beam)
 hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p, hipStream_t s,
@@ -186,6 +206,15 @@ hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int
 // per-edge distances of slots [0, n) of an imported / loaded graph (levels: per slot)
 hipError_t launch_edge_dist_fill(Storage st, MetricKind mk, const DevGraph& g, const int8_t* levels, size_t n,
                                  hipStream_t s);
+// slot reuse (hnsw.hip): stage n reused slots (prepared rows | |x|^2 | keys ->
+// their slots; rows of every level cleared; flags = removed | relink), then
+// refresh the stored distances of links into them (slots [0, n) scanned;
+// levels: per slot)
+hipError_t launch_reuse_stage(const DevGraph& g, uint8_t* vecs, float* sqnorm, uint64_t* keys_out, uint8_t* flags,
+                              const uint8_t* rows, const float* sq, const uint64_t* keys, const uint32_t* slots,
+                              const int8_t* levels, size_t n, hipStream_t s);
+hipError_t launch_edge_dist_refresh(Storage st, MetricKind mk, const DevGraph& g, const int8_t* levels,
+                                    const uint8_t* flags, size_t n, hipStream_t s);
 hipError_t launch_exact(Storage st, MetricKind mk, const ExactParams& p, hipStream_t s);
 hipError_t launch_merge_parts(const MergeParams& p, hipStream_t s);
 hipError_t launch_rerank(MetricKind mk, const RerankParams& p, hipStream_t s);

@@ -70,6 +70,14 @@ class Stats(C.Structure):
         ("build_reverse_ns", C.c_uint64),
         ("build_select_ns", C.c_uint64),
         ("search_filter_overflow", C.c_uint64),
+        ("search_filter_reruns", C.c_uint64),
+        ("slots_reused", C.c_uint64),
+        ("ktile_copy_failures", C.c_uint64),
+        ("host_searches", C.c_uint64),
+        ("host_search_ns", C.c_uint64),
+        ("host_h2d_ns", C.c_uint64),
+        ("host_device_ns", C.c_uint64),
+        ("host_d2h_ns", C.c_uint64),
     ]
 
 
@@ -115,7 +123,8 @@ class ActorCounters(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in (
         "messages", "writes", "anns", "counts", "add_calls", "remove_calls", "search_calls",
         "reserve_calls", "add_errors", "remove_errors", "search_errors", "max_search_batch",
-        "max_add_batch", "compactions", "compacted_rows", "compact_errors")]
+        "max_add_batch", "compactions", "compacted_rows", "compact_errors",
+        "ann_queue_ns", "ann_wake_ns", "batch_search_ns", "batch_notify_ns")]
 
 
 _lib = None
@@ -154,6 +163,7 @@ def lib() -> C.CDLL:
         "vsg_index_add": (C.c_int, [P, P, P, sz]),
         "vsg_index_add_device": (C.c_int, [P, P, P, sz, P]),
         "vsg_index_remove": (C.c_int, [P, P, sz, C.POINTER(sz)]),
+        "vsg_index_free_slots": (sz, [P, P, sz]),
         "vsg_index_search": (C.c_int, [P, P, sz, sz, sz, P, P, P]),
         "vsg_index_exact_search": (C.c_int, [P, P, sz, sz, P, P, P]),
         "vsg_index_search_device": (C.c_int, [P, P, sz, sz, sz, P, P, P, P]),

@@ -29,15 +29,18 @@ class Actor:
                  connectivity: int = 0, expansion_add: int = 0, expansion_search: int = 0,
                  device: int = 0, seed: int = 0, reserve_increment: int = 0, reserve_threshold: int = 0,
                  max_batch: int = 0, max_wait_us: int = 0, compact_percent: int = 0, compact_min_dead: int = 0,
-                 f16_traversal: bool = False, concurrent_reads: int = 0, devices=None):
+                 f16_traversal: bool = False, concurrent_reads: int = 0, devices=None,
+                 slot_reuse: bool = True):
         """devices: a list of device ordinals => one shard per entry (vsg_actor_new_sharded,
         include/vsg.h "Sharded index"); None => one index on `device`.
         concurrent_reads: 0 (or False) = submission order; n (or True = 1) = n read workers
-        beside the writes (n >= 2: n search batches in flight)."""
+        beside the writes (n >= 2: n search batches in flight).
+        slot_reuse: False => VSG_FLAG_NO_SLOT_REUSE (append-only adds; compaction reclaims)."""
         self.dimensions = int(dimensions)
         # f16_traversal: opt-in VSG_FLAG_F16_TRAVERSAL (f16 walk + exact f32 re-rank, DESIGN.md §3.5)
         opt = ActorOptions(Options(self.dimensions, METRICS[metric], SCALARS[quantization], connectivity,
-                                   expansion_add, expansion_search, device, 2 if f16_traversal else 0, seed),
+                                   expansion_add, expansion_search, device,
+                                   (2 if f16_traversal else 0) | (0 if slot_reuse else 4), seed),
                            reserve_increment, reserve_threshold, max_batch, max_wait_us, compact_percent,
                            int(concurrent_reads), compact_min_dead)
         h = C.c_void_p()

@@ -51,13 +51,13 @@ class Index:
     def __init__(self, dimensions: int, metric: str = "l2sq", quantization: str = "f32",
                  connectivity: int = 0, expansion_add: int = 0, expansion_search: int = 0,
                  device: int = 0, seed: int = 0, exact_only: bool = False,
-                 f16_traversal: bool = False):
+                 f16_traversal: bool = False, slot_reuse: bool = True):
         self.dimensions = int(dimensions)
         self.metric = metric
         self.quantization = quantization
         opt = Options(self.dimensions, METRICS[metric], SCALARS[quantization], connectivity,
                       expansion_add, expansion_search, device,
-                      (1 if exact_only else 0) | (2 if f16_traversal else 0), seed)
+                      (1 if exact_only else 0) | (2 if f16_traversal else 0) | (0 if slot_reuse else 4), seed)
         h = C.c_void_p()
         check(lib().vsg_index_new(C.byref(opt), C.byref(h)))
         self._h = h
@@ -110,6 +110,14 @@ class Index:
         n = C.c_size_t()
         check(lib().vsg_index_remove(self._h, _p(keys), len(keys), C.byref(n)))
         return n.value
+
+    def free_slots(self) -> np.ndarray:
+        """The free ring (usearch index_dense free_keys_): removed slots, oldest removal
+        first; the next adds re-link them in this order."""
+        n = lib().vsg_index_free_slots(self._h, None, 0)
+        out = np.empty(n, np.uint32)
+        n2 = lib().vsg_index_free_slots(self._h, _p(out), n)
+        return out[:min(n, n2)]
 
     def _search(self, queries, k, ef, exact):
         q = np.ascontiguousarray(queries, np.float32).reshape(-1, self.dimensions)

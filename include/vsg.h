@@ -395,6 +395,18 @@ int vsg_actor_remove(vsg_actor_t* actor, uint64_t key);
  * past *out_count. */
 int vsg_actor_ann(vsg_actor_t* actor, const float* embedding, size_t dims, size_t limit,
                   uint64_t* out_keys, float* out_distances, size_t* out_count);
+/* Index::Ann with a completion instead of a blocked thread -- the C form of the
+ * reference's oneshot reply (usearch.rs:251-306: `ann` sends the query with a
+ * oneshot::Sender and the caller awaits the receiver).  Same checks and batching as
+ * vsg_actor_ann; returns at once.  `done(ctx, status, count)` runs on an actor worker
+ * thread once the batched search carrying this query finished, after out_keys /
+ * out_distances (`limit` entries each, caller-owned until then, ascending, padded
+ * past count) were written; on failure status is the search's error and
+ * vsg_last_error() inside the callback holds its message.  The callback may submit
+ * further messages; it must not block on the actor. */
+typedef void (*vsg_ann_done_fn)(void* ctx, int status, size_t count);
+int vsg_actor_ann_cb(vsg_actor_t* actor, const float* embedding, size_t dims, size_t limit,
+                     uint64_t* out_keys, float* out_distances, vsg_ann_done_fn done, void* ctx);
 /* Index::Count — usearch.rs:308-311 (live size) */
 int vsg_actor_count(vsg_actor_t* actor, size_t* out);
 /* Index::Count as the reference computes it (usearch.rs:308-311: a read-lock

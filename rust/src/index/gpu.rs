@@ -26,8 +26,14 @@
 //!
 //! Symbol sequence a lifecycle drives (mirrored by tests/cpp/test_rust_call_sequence.cpp):
 //!   vsg_actor_new | vsg_actor_new_sharded (index(es) + reserve(1M)) ->
-//!   vsg_actor_add_or_replace_cb* -> vsg_actor_remove -> vsg_actor_ann -> vsg_actor_size ->
+//!   vsg_actor_add_or_replace_cb* -> vsg_actor_remove -> vsg_actor_ann_cb -> vsg_actor_size ->
 //!   vsg_actor_free.
+//!
+//! Ann is asynchronous end to end (round 5): `vsg_actor_ann_cb` queues the query and its
+//! completion `ann_done` -- run on the native worker once the batched GPU search returned --
+//! maps the keys and sends the oneshot reply, as the reference's `ann` answers through a
+//! oneshot (usearch.rs:251-306).  No thread blocks per query (round 4 parked a
+//! `spawn_blocking` thread in `vsg_actor_ann` for every in-flight query).
 
 use crate::Connectivity;
 use crate::Dimensions;
@@ -92,6 +98,35 @@ unsafe extern "C" fn add_done(ctx: *mut c_void, key: u64, status: c_int) {
     keys.write().unwrap().map.remove_by_right(&key);
 }
 
+/// One ann in flight: its reply channel and the buffers the native actor fills before
+/// `ann_done` runs (heap-owned, so the pointers stay valid while the query is queued).
+struct AnnCtx {
+    tx: Option<oneshot::Sender<AnnR>>,
+    keys: Keys,
+    out_keys: Vec<u64>,
+    out_dist: Vec<f32>,
+}
+
+/// Completion of one ann (a native worker thread): keys -> primary keys (usearch.rs:285-296),
+/// distances (:297-301), the oneshot reply.  On failure vsg_last_error() is the search's.
+unsafe extern "C" fn ann_done(ctx: *mut c_void, status: c_int, count: usize) {
+    let mut c = unsafe { Box::from_raw(ctx as *mut AnnCtx) };
+    let result = if status != sys::VSG_OK {
+        let msg = unsafe { CStr::from_ptr(sys::vsg_last_error()) }.to_string_lossy().into_owned();
+        Err(anyhow!("ann: search failed: vsg error {status}: {msg}"))
+    } else {
+        let k = c.keys.read().unwrap();
+        c.out_keys[..count]
+            .iter()
+            .map(|key| k.map.get_by_right(key).cloned().ok_or(anyhow!("not defined primary key column {key}")))
+            .collect::<anyhow::Result<Vec<_>>>()
+            .map(|pks| (pks, c.out_dist[..count].iter().map(|d| (*d).into()).collect()))
+    };
+    if let Some(tx) = c.tx.take() {
+        tx.send(result).unwrap_or_else(|_| trace!("ann: unable to send response"));
+    }
+}
+
 impl GpuActor {
     fn new(options: &sys::vsg_actor_options_t, devices: &[i32], keys: Keys) -> anyhow::Result<Self> {
         let mut a = std::ptr::null_mut();
@@ -114,18 +149,27 @@ impl GpuActor {
         check(unsafe { sys::vsg_actor_remove(self.ptr, key) })
     }
 
-    /// Blocks until the batched search holding this query returns.
-    fn ann(&self, embedding: &[f32], limit: usize) -> anyhow::Result<(Vec<u64>, Vec<f32>)> {
-        let mut keys = vec![sys::VSG_NO_KEY; limit];
-        let mut distances = vec![f32::INFINITY; limit];
-        let mut n = 0usize;
-        check(unsafe {
-            sys::vsg_actor_ann(self.ptr, embedding.as_ptr(), embedding.len(), limit, keys.as_mut_ptr(),
-                               distances.as_mut_ptr(), &mut n)
-        })?;
-        keys.truncate(n);
-        distances.truncate(n);
-        Ok((keys, distances))
+    /// Queues the query; `ann_done` sends the reply on `tx` once its batch returned.
+    fn ann(&self, embedding: &[f32], limit: usize, tx: oneshot::Sender<AnnR>) {
+        let mut ctx = Box::new(AnnCtx {
+            tx: Some(tx),
+            keys: Arc::clone(&self.keys),
+            out_keys: vec![sys::VSG_NO_KEY; limit],
+            out_dist: vec![f32::INFINITY; limit],
+        });
+        let (ok, od) = (ctx.out_keys.as_mut_ptr(), ctx.out_dist.as_mut_ptr());
+        let raw = Box::into_raw(ctx);
+        let rc = unsafe {
+            sys::vsg_actor_ann_cb(self.ptr, embedding.as_ptr(), embedding.len(), limit, ok, od, Some(ann_done),
+                                  raw as *mut c_void)
+        };
+        if let Err(err) = check(rc) {
+            // not queued: the completion will not run, the reply goes out here
+            ctx = unsafe { Box::from_raw(raw) };
+            if let Some(tx) = ctx.tx.take() {
+                tx.send(Err(anyhow!("ann: search failed: {err}"))).unwrap_or_else(|_| trace!("ann: unable to send response"));
+            }
+        }
     }
 
     /// live size now, under the index's shared lock (does not wait for queued writes)
@@ -211,9 +255,11 @@ pub(crate) fn new(
         // reserve(RESERVE_INCREMENT) up front and the growth rule of usearch.rs:200-212
         reserve_increment: 1_000_000,
         reserve_threshold: 1_000_000 / 3,
-        // anns beside writes, as the reference's fire-and-forget adds allow, on two
-        // read workers: two search batches in flight overlap one's GPU tail with the next
-        concurrent_reads: 2,
+        // anns on one read worker beside the writes, as the reference's fire-and-forget
+        // adds allow.  With completions (vsg_actor_ann_cb) one worker keeps the batches
+        // largest: 512 closed-loop clients 640 k QPS on 1, 482 k on 2, 448 k on 3 read
+        // workers (profiles/r05_actor_completions.jsonl)
+        concurrent_reads: 1,
         ..Default::default()
     };
     let keys: Keys = Arc::new(RwLock::new(KeyMap { map: BiMap::new(), next: 0 }));
@@ -236,10 +282,8 @@ async fn process(msg: Index, dimensions: Dimensions, actor: Arc<GpuActor>, keys:
     match msg {
         Index::AddOrReplace { primary_key, embedding } => add_or_replace(&actor, &keys, primary_key, embedding),
         Index::Remove { primary_key } => remove(&actor, &keys, primary_key),
-        // the native call blocks until its batch is answered: off the async runtime
-        Index::Ann { embedding, limit, tx } => {
-            tokio::task::spawn_blocking(move || ann(&actor, &keys, tx, embedding, dimensions, limit));
-        }
+        // queued with a completion: the reply is sent from the native worker (ann_done)
+        Index::Ann { embedding, limit, tx } => ann(&actor, tx, embedding, dimensions, limit),
         Index::Count { tx } => count(&actor, tx),
     }
 }
@@ -277,27 +321,20 @@ fn remove(actor: &GpuActor, keys: &Keys, primary_key: PrimaryKey) {
     }
 }
 
-/// usearch.rs:251-306: dimension checks, search, keys -> primary keys, distances.
-fn ann(actor: &GpuActor, keys: &Keys, tx: oneshot::Sender<AnnR>, embedding: Embedding, dimensions: Dimensions,
-       limit: Limit) {
-    let result = (|| {
-        let len = embedding.0.len();
-        if len == 0 {
-            return Err(anyhow!("ann: embedding dimensions == 0"));
-        }
-        if len != dimensions.0.get() {
-            return Err(anyhow!("ann: wrong embedding dimensions: {len} != {dimensions}"));
-        }
-        let (found, distances) =
-            actor.ann(&embedding.0, limit.0.get()).map_err(|err| anyhow!("ann: search failed: {err}"))?;
-        let k = keys.read().unwrap();
-        let primary_keys = found
-            .into_iter()
-            .map(|key| k.map.get_by_right(&key).cloned().ok_or(anyhow!("not defined primary key column {key}")))
-            .collect::<anyhow::Result<_>>()?;
-        Ok((primary_keys, distances.into_iter().map(|d| d.into()).collect()))
-    })();
-    tx.send(result).unwrap_or_else(|_| trace!("ann: unable to send response"));
+/// usearch.rs:251-306: dimension checks here (:259-272), then the batched search; the
+/// key -> primary key mapping and the reply happen in `ann_done`.
+fn ann(actor: &GpuActor, tx: oneshot::Sender<AnnR>, embedding: Embedding, dimensions: Dimensions, limit: Limit) {
+    let len = embedding.0.len();
+    if len == 0 {
+        tx.send(Err(anyhow!("ann: embedding dimensions == 0"))).unwrap_or_else(|_| trace!("ann: unable to send response"));
+        return;
+    }
+    if len != dimensions.0.get() {
+        tx.send(Err(anyhow!("ann: wrong embedding dimensions: {len} != {dimensions}")))
+            .unwrap_or_else(|_| trace!("ann: unable to send response"));
+        return;
+    }
+    actor.ann(&embedding.0, limit.0.get(), tx);
 }
 
 /// usearch.rs:308-311: the live size under a read lock, answered at once

@@ -141,6 +141,8 @@ pub struct vsg_sharded_options_t {
 
 /// Completion of one AddOrReplace (vsg_actor_add_or_replace_cb), on the actor's worker thread.
 pub type vsg_add_done_fn = Option<unsafe extern "C" fn(ctx: *mut c_void, key: u64, status: c_int)>;
+/// Completion of one Ann (vsg_actor_ann_cb), on an actor worker thread: the oneshot reply.
+pub type vsg_ann_done_fn = Option<unsafe extern "C" fn(ctx: *mut c_void, status: c_int, count: usize)>;
 
 #[repr(C)]
 #[derive(Clone, Copy, Debug, Default)]
@@ -234,6 +236,9 @@ extern "C" {
     pub fn vsg_actor_add_or_replace(actor: *mut vsg_actor_t, key: u64, embedding: *const f32, dims: usize) -> c_int;
     pub fn vsg_actor_add_or_replace_cb(actor: *mut vsg_actor_t, key: u64, embedding: *const f32, dims: usize,
                                        done: vsg_add_done_fn, ctx: *mut c_void) -> c_int;
+    pub fn vsg_actor_ann_cb(actor: *mut vsg_actor_t, embedding: *const f32, dims: usize, limit: usize,
+                            out_keys: *mut u64, out_distances: *mut f32, done: vsg_ann_done_fn,
+                            ctx: *mut c_void) -> c_int;
     pub fn vsg_actor_size(actor: *const vsg_actor_t) -> usize;
     pub fn vsg_actor_remove(actor: *mut vsg_actor_t, key: u64) -> c_int;
     pub fn vsg_actor_ann(actor: *mut vsg_actor_t, embedding: *const f32, dims: usize, limit: usize,

@@ -185,6 +185,72 @@ static void test_concurrent_anns() {
     CHECK(c.max_search_batch > 1);
 }
 
+// 2b) anns with completions (ann_cb, the oneshot form): a closed loop of 64 clients
+//     driven only from the callbacks answers like the exact scan, batched, with every
+//     completion run once; a rejected query gets no completion.
+struct CbCtx {
+    vsg::Actor* a;
+    int client, i;
+    std::vector<uint64_t> keys;
+    std::vector<float> dist;
+    std::atomic<int>* bad;
+    std::atomic<int>* finished;
+};
+static std::vector<float> cb_query(int client, int i) { return vec_of(9000 + client * 100 + i, 8); }
+static void cb_done(void* p, int status, size_t cnt) {
+    auto* c = static_cast<CbCtx*>(p);
+    auto q = cb_query(c->client, c->i);
+    std::vector<std::pair<float, uint64_t>> all;
+    for (uint64_t r = 0; r < 500; ++r) {
+        auto v = vec_of(r + 100, 8);
+        float s = 0;
+        for (int d = 0; d < 8; ++d) s += (v[d] - q[d]) * (v[d] - q[d]);
+        all.push_back({s, r});
+    }
+    std::sort(all.begin(), all.end());
+    if (status != 0 || cnt != c->keys.size()) (*c->bad)++;
+    for (size_t j = 0; j < c->keys.size(); ++j)
+        if (c->keys[j] != all[j].second || c->dist[j] != all[j].first) (*c->bad)++;
+    if (++c->i < 20) {
+        auto nq = cb_query(c->client, c->i);
+        if (c->a->ann_cb(nq.data(), 8, c->keys.size(), c->keys.data(), c->dist.data(), cb_done, c) != 0) (*c->bad)++;
+        return;
+    }
+    (*c->finished)++;
+}
+static void test_ann_completions() {
+    std::vector<Call> log;
+    std::vector<size_t> res;
+    auto* m = new Mock(8, 16, &log, &res, 2000);
+    vsg::ActorConfig cfg;
+    cfg.concurrent_reads = 2;
+    vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), cfg);
+    CHECK(a.init() == 0);
+    for (uint64_t k = 0; k < 500; ++k) {
+        auto v = vec_of(k + 100, 8);
+        a.add_or_replace(k, v.data());
+    }
+    CHECK(a.flush() == 0);
+    std::atomic<int> bad{0}, finished{0};
+    const int C = 64;
+    std::vector<CbCtx> cl(C);
+    for (int t = 0; t < C; ++t) {
+        cl[t] = CbCtx{&a, t, 0, std::vector<uint64_t>(1 + t % 10), std::vector<float>(1 + t % 10), &bad, &finished};
+        auto q = cb_query(t, 0);
+        CHECK(a.ann_cb(q.data(), 8, cl[t].keys.size(), cl[t].keys.data(), cl[t].dist.data(), cb_done, &cl[t]) == 0);
+    }
+    for (int w = 0; w < 2000 && finished.load() < C; ++w) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    CHECK(finished.load() == C);
+    CHECK(bad == 0);
+    const auto c = a.counters();
+    CHECK(c.anns == (uint64_t)(C * 20));
+    CHECK(c.search_calls < c.anns);  // batched
+    uint64_t kk[1];
+    float dd[1];
+    auto q = cb_query(0, 0);
+    CHECK(a.ann_cb(q.data(), 3, 1, kk, dd, cb_done, nullptr) == 1);  // wrong dims: rejected, no completion
+}
+
 // 3) effective-ef grouping: one drained run with k below and above ef0 makes
 //    two searches, each at ef = max(ef0, k); wrong dims are rejected up front.
 static void test_ef_groups_and_errors() {
@@ -517,6 +583,7 @@ int main() {
     test_read_workers_overlap();
     test_fifo_semantics();
     test_concurrent_anns();
+    test_ann_completions();
     test_ef_groups_and_errors();
     test_add_errors_swallowed();
     test_add_completions();

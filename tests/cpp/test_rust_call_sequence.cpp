@@ -6,17 +6,20 @@
 //     vsg_index_new -> vsg_index_reserve(1M) -> vsg_index_add -> replace
 //     (vsg_index_remove + vsg_index_add of the same key) -> vsg_index_search ->
 //     vsg_index_size -> vsg_index_free;
-//  2. the actor path gpu.rs uses (vsg_actor_*, concurrent_reads = 2): the reference's own
+//  2. the actor path gpu.rs uses (vsg_actor_*, concurrent_reads = 1): the reference's own
 //     unit KAT (usearch.rs:322-425, D = 3, keys 1/2/3, replace, remove, count) with its
 //     polling (anns may run before earlier writes land, as the reference's fire-and-forget
 //     adds allow; it polls for 10 s, usearch.rs:352-358).  Adds go through
 //     vsg_actor_add_or_replace_cb (gpu.rs rolls the BiMap back from the completion,
-//     usearch.rs:230-232), counts through vsg_actor_size (usearch.rs:308-311).  Run once
+//     usearch.rs:230-232), anns through vsg_actor_ann_cb (gpu.rs sends the oneshot reply
+//     from the completion, round 5), counts through vsg_actor_size (usearch.rs:308-311).  Run once
 //     on a one-device actor (new_gpu) and once on a two-shard actor on device 0
 //     (new_gpu_sharded(&[0, 0]), vsg_actor_new_sharded).
 // Metric l2sq: the KAT is an f32 rounding tie under cosine.
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <thread>
@@ -61,6 +64,32 @@ static void direct_index() {
     vsg_index_free(h);
 }
 
+// gpu.rs ann: vsg_actor_ann_cb, the reply arrives in the completion (a oneshot here)
+struct AnnReply {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false;
+    int status = -1;
+    size_t count = 0;
+};
+static void ann_done(void* ctx, int status, size_t count) {
+    auto* r = static_cast<AnnReply*>(ctx);
+    std::lock_guard<std::mutex> lk(r->m);
+    r->status = status;
+    r->count = count;
+    r->done = true;
+    r->cv.notify_all();
+}
+static int ann_cb(vsg_actor_t* a, const float* q, size_t dims, size_t limit, uint64_t* k, float* d, size_t* n) {
+    AnnReply r;
+    const int rc = vsg_actor_ann_cb(a, q, dims, limit, k, d, ann_done, &r);
+    if (rc != VSG_OK) return rc;  // rejected: no completion
+    std::unique_lock<std::mutex> lk(r.m);
+    r.cv.wait(lk, [&] { return r.done; });
+    *n = r.count;
+    return r.status;
+}
+
 // poll an ann until it returns `want` (or 10 s), as the reference test does
 static bool ann_becomes(vsg_actor_t* a, const float* q, uint64_t want) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -68,7 +97,7 @@ static bool ann_becomes(vsg_actor_t* a, const float* q, uint64_t want) {
         uint64_t k = 0;
         float d = 0;
         size_t n = 0;
-        if (vsg_actor_ann(a, q, 3, 1, &k, &d, &n) != VSG_OK) return false;
+        if (ann_cb(a, q, 3, 1, &k, &d, &n) != VSG_OK) return false;
         if (n == 1 && k == want) return true;
         std::this_thread::sleep_for(std::chrono::milliseconds(1));
     }
@@ -98,7 +127,7 @@ static void actor_kat(bool sharded) {
     o.index.metric = VSG_METRIC_L2SQ;
     o.reserve_increment = 1000000;  // RESERVE_INCREMENT, usearch.rs:62
     o.reserve_threshold = 1000000 / 3;
-    o.concurrent_reads = 2;  // as rust/src/index/gpu.rs
+    o.concurrent_reads = 1;  // as rust/src/index/gpu.rs
     vsg_actor_t* a = nullptr;
     const int32_t devs[2] = {0, 0};
     if (sharded) {
@@ -128,8 +157,9 @@ static void actor_kat(bool sharded) {
     uint64_t k;
     float d;
     size_t n;
-    CHECK(vsg_actor_ann(a, q, 2, 1, &k, &d, &n) == VSG_EINVAL);
-    CHECK(vsg_actor_ann(a, q, 3, 0, &k, &d, &n) == VSG_EINVAL);
+    CHECK(ann_cb(a, q, 2, 1, &k, &d, &n) == VSG_EINVAL);
+    CHECK(ann_cb(a, q, 3, 0, &k, &d, &n) == VSG_EINVAL);
+    CHECK(vsg_actor_ann(a, q, 2, 1, &k, &d, &n) == VSG_EINVAL);  // the blocking form checks the same
     CHECK(vsg_actor_flush(a) == VSG_OK);
     vsg_actor_counters_t c{};
     CHECK(vsg_actor_counters(a, &c) == VSG_OK && c.add_errors == 0);

@@ -8,12 +8,17 @@
 // build: make -C tools actor_load   (links ../vector-store-text_amd/lib/libvsg.so)
 // usage: actor_load rows dim metric(0 l2sq,1 ip,2 cos) clients queries_per_client k ef [max_wait_us]
 //        [read_workers: 0 = anns on the one FIFO worker; n = concurrent_reads n]
+//        [mode: 0 = one OS thread per client blocked in vsg_actor_ann; 1 = clients as
+//         completions (vsg_actor_ann_cb, the reference's oneshot reply): each finished
+//         query submits that client's next one from its callback -- no thread per client]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <mutex>
 #include <cstdlib>
 #include <thread>
 #include <vector>
@@ -42,6 +47,7 @@ int main(int argc, char** argv) {
     const size_t k = std::strtoull(argv[6], nullptr, 10), ef = std::strtoull(argv[7], nullptr, 10);
     const unsigned wait_us = argc > 8 ? (unsigned)std::atoi(argv[8]) : 0;
     const unsigned readers = argc > 9 ? (unsigned)std::atoi(argv[9]) : 0;
+    const int mode = argc > 10 ? std::atoi(argv[10]) : 0;
     const uint64_t cfg = 2, base_seed = 0x5EED0000 + cfg, q_seed = 0x5EED1000 + cfg, m_seed = 0x5EED2000 + cfg;
 
     vsg_actor_options_t o{};
@@ -115,10 +121,78 @@ int main(int argc, char** argv) {
                 }
         }
     };
+    // callback clients: client t's i-th query is qi = i * clients + t, submitted from the
+    // completion of its (i-1)-th; outputs per client, checked in the completion
+    struct CbClient {
+        void* owner = nullptr;  // the CbRun
+        int t = 0, i = 0;
+        clk::time_point s;
+        std::vector<uint64_t> ok;
+        std::vector<float> od;
+    };
+    struct CbRun {
+        vsg_actor_t* a;
+        const float* q;
+        size_t dim, k;
+        int clients, qpc;
+        std::vector<CbClient> cl;
+        std::vector<double>* lat;
+        std::vector<uint64_t>* ak;
+        const std::vector<uint64_t>* bk;
+        const std::vector<float>* bd;
+        std::atomic<int>* mismatch;
+        std::atomic<int>* errors;
+        std::atomic<size_t> finished{0};
+        std::mutex m;
+        std::condition_variable cv;
+    } run{a, q.data(), dim, k, clients, qpc, {}, &lat, &ak, &bk, &bd, &mismatch, &errors};
+    struct Cb {
+        static int submit(CbRun* r, CbClient* c) {
+            const size_t qi = (size_t)c->i * r->clients + c->t;
+            c->s = clk::now();
+            return vsg_actor_ann_cb(r->a, r->q + qi * r->dim, r->dim, r->k, c->ok.data(), c->od.data(), done,
+                                    (void*)c);
+        }
+        static void done(void* ctx, int status, size_t) {
+            CbClient* c = static_cast<CbClient*>(ctx);
+            CbRun* r = static_cast<CbRun*>(c->owner);
+            const size_t qi = (size_t)c->i * r->clients + c->t;
+            if (status) {
+                (*r->errors)++;
+            } else {
+                (*r->lat)[qi] = std::chrono::duration<double, std::micro>(clk::now() - c->s).count();
+                std::copy(c->ok.begin(), c->ok.end(), r->ak->begin() + qi * r->k);
+                for (size_t j = 0; j < r->k; ++j)
+                    if (c->ok[j] != (*r->bk)[qi * r->k + j] || c->od[j] != (*r->bd)[qi * r->k + j]) {
+                        (*r->mismatch)++;
+                        break;
+                    }
+            }
+            if (++c->i < r->qpc && submit(r, c) == VSG_OK) return;
+            if (c->i < r->qpc) (*r->errors)++;
+            if (++r->finished == (size_t)r->clients) {
+                std::lock_guard<std::mutex> lk(r->m);
+                r->cv.notify_all();
+            }
+        }
+    };
     std::vector<std::thread> th;
     t0 = clk::now();
-    for (int t = 0; t < clients; ++t) th.emplace_back(client, t);
-    for (auto& x : th) x.join();
+    if (mode == 1) {
+        run.cl.resize(clients);
+        for (int t = 0; t < clients; ++t) {
+            run.cl[t].owner = &run;
+            run.cl[t].t = t;
+            run.cl[t].ok.assign(k, 0);
+            run.cl[t].od.assign(k, 0.f);
+        }
+        for (int t = 0; t < clients; ++t) TRY(Cb::submit(&run, &run.cl[t]));
+        std::unique_lock<std::mutex> lk(run.m);
+        run.cv.wait(lk, [&] { return run.finished.load() == (size_t)clients; });
+    } else {
+        for (int t = 0; t < clients; ++t) th.emplace_back(client, t);
+        for (auto& x : th) x.join();
+    }
     const double served_s = std::chrono::duration<double>(clk::now() - t0).count();
     vsg_actor_counters_t c1{};
     vsg_actor_counters(a, &c1);
@@ -172,10 +246,10 @@ int main(int argc, char** argv) {
                  (s1.host_device_ns - s0.host_device_ns) / 1e3 / hs, (s1.host_d2h_ns - s0.host_d2h_ns) / 1e3 / hs);
     std::printf(
         "{\"rows\": %zu, \"dim\": %zu, \"clients\": %d, \"queries\": %zu, \"k\": %zu, \"ef\": %zu, "
-        "\"max_wait_us\": %u, \"read_workers\": %u, \"actor_qps\": %.1f, \"batched_qps\": %.1f, \"lat_us_p50\": %.1f, "
+        "\"max_wait_us\": %u, \"read_workers\": %u, \"clients_as\": \"%s\", \"actor_qps\": %.1f, \"batched_qps\": %.1f, \"lat_us_p50\": %.1f, "
         "\"lat_us_p99\": %.1f, \"search_calls\": %llu, \"mean_batch\": %.1f, \"max_batch\": %llu, "
         "\"mismatch_vs_batched\": %d, \"errors\": %d}\n",
-        rows, dim, clients, nq, k, ef, wait_us, readers, nq / served_s, nq / batched_s, lat[nq / 2], lat[nq * 99 / 100],
+        rows, dim, clients, nq, k, ef, wait_us, readers, mode == 1 ? "completions" : "threads", nq / served_s, nq / batched_s, lat[nq / 2], lat[nq * 99 / 100],
         (unsigned long long)calls, calls ? (double)nq / calls : 0.0, (unsigned long long)c1.max_search_batch,
         mismatch.load(), errors.load());
     vsg_actor_free(a);

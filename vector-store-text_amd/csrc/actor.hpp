@@ -31,6 +31,7 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -140,6 +141,10 @@ class Actor {
         uint64_t key = 0;
         size_t k = 0;
         uint64_t t_enq = 0;  // steady_ns() at submission
+        // ann_cb: outputs and completion (w == nullptr)
+        uint64_t* out_keys = nullptr;
+        float* out_dist = nullptr;
+        void (*ann_done)(void* ctx, int status, size_t count) = nullptr;
         std::vector<float> vec;
         Waiter* w = nullptr;
         AddDone done = nullptr;
@@ -207,6 +212,26 @@ class Actor {
         if (count) *count = w.count;
         if (err) *err = w.err;
         return rc;
+    }
+
+    // Index::Ann with a completion instead of a blocked thread: the C form of the
+    // reference's oneshot reply (usearch.rs:251-306: the caller awaits a
+    // oneshot::Receiver).  done(ctx, status, count) runs on the worker thread once
+    // the batched search carrying this query finished, after keys / dist (limit
+    // entries, ascending, padded) were written -- no thread wake-up per query.
+    using AnnDone = void (*)(void* ctx, int status, size_t count);
+    int ann_cb(const float* q, size_t dims, size_t k, uint64_t* keys, float* dist, AnnDone done, void* ctx) {
+        if (k == 0 || dims != be_->dimensions() || !done) return 1;  // VSG_EINVAL
+        Msg m;
+        m.kind = ANN;
+        m.k = k;
+        m.vec.assign(q, q + dims);
+        m.out_keys = keys;
+        m.out_dist = dist;
+        m.ann_done = done;
+        m.done_ctx = ctx;
+        push(std::move(m));
+        return 0;
     }
 
     // Index::Count
@@ -440,21 +465,28 @@ class Actor {
                 if (rc) ctr_.search_errors += g.size();
                 ctr_.batch_search_ns += tn - ts;
             }
+            const std::string err = rc ? be_->last_error() : std::string();
             for (size_t r = 0; r < g.size(); ++r) {
                 Msg& m = b[g[r]];
+                uint64_t* ok = m.w ? m.w->keys : m.out_keys;
+                float* od = m.w ? m.w->dist : m.out_dist;
+                size_t c = 0;
                 if (rc == 0) {
-                    const size_t c = std::min(counts[r], m.k);
-                    std::memcpy(m.w->keys, &keys[r * kmax], c * 8);
-                    std::memcpy(m.w->dist, &dist[r * kmax], c * 4);
+                    c = std::min(counts[r], m.k);
+                    std::memcpy(ok, &keys[r * kmax], c * 8);
+                    std::memcpy(od, &dist[r * kmax], c * 4);
                     for (size_t t = c; t < m.k; ++t) {
-                        m.w->keys[t] = ~0ull;
-                        m.w->dist[t] = __builtin_inff();
+                        ok[t] = ~0ull;
+                        od[t] = __builtin_inff();
                     }
-                    m.w->count = c;
-                } else {
-                    m.w->err = be_->last_error();
                 }
-                m.w->finish(rc);
+                if (m.w) {  // a blocked caller (ann): wake it
+                    if (rc == 0) m.w->count = c;
+                    else m.w->err = err;
+                    m.w->finish(rc);
+                } else {  // ann_cb: the completion runs here, like a oneshot send
+                    m.ann_done(m.done_ctx, rc, c);
+                }
             }
             const uint64_t dn = steady_ns() - tn;
             std::lock_guard<std::mutex> lk(cm_);

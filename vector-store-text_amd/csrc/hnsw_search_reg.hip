@@ -158,6 +158,11 @@ static inline int reg_rows(int ef) { return ef <= 64 ? 2 : ef <= 192 ? 4 : ef <=
 
 size_t search_reg_lds_bytes(int hash) { return wave_lds_bytes(hash, 0, 0); }
 
+static double env_frac(const char* name, double dflt) {
+    const char* e = getenv(name);
+    return e ? atof(e) : dflt;
+}
+
 // one-wave workgroups of `kern` resident on the whole device at `lds` bytes each
 // (occupancy x CUs), cached per (device, kernel, lds)
 static int resident_blocks(const void* kern, size_t lds) {
@@ -205,7 +210,13 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
                 c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
                 unsigned grid = (unsigned)c.nq;
                 if (p.qnext) {  // persistent: one round of resident waves, counter reset per launch
-                    grid = (unsigned)std::max(1, std::min(c.nq, resident_blocks((const void*)kern, lds)));
+                    // half of the resident waves: at C2 the kernel is throughput-bound from
+                    // ~0.35 of the occupancy on, and fewer waves end the batch sooner (fractions
+                    // 0.25 / 0.35 / 0.5 / 0.6 / 1.0: 3.20 / 3.35 / 3.34 / 3.34 / 3.28 M QPS,
+                    // profiles/r05_pfrac.jsonl); VSG_SEARCH_PERSIST_FRAC overrides (probes)
+                    static const double frac = std::min(1.0, std::max(0.05, env_frac("VSG_SEARCH_PERSIST_FRAC", 0.5)));
+                    const int res = std::max(1, (int)(frac * resident_blocks((const void*)kern, lds)));
+                    grid = (unsigned)std::max(1, std::min(c.nq, res));
                     err = hipMemsetAsync(p.qnext, 0, sizeof(unsigned), s);
                     if (err != hipSuccess) break;
                 }

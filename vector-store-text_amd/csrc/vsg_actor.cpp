@@ -1,6 +1,7 @@
 // vsg_actor.cpp — C ABI of the index actor (include/vsg.h, "Actor" section):
 // the GPU index behind the reference's message API (src/index/usearch.rs
 // :82-311), with request coalescing (csrc/actor.hpp).
+#include <cstdlib>
 #include <string>
 
 #include "../../include/vsg.h"
@@ -202,6 +203,20 @@ int vsg_actor_ann(vsg_actor_t* a, const float* embedding, size_t dims, size_t li
     const int rc = a->actor->ann(embedding, dims, limit, out_keys, out_distances, out_count, &err);
     if (rc) return actor_fail(rc, "ann: search failed: " + err);
     return VSG_OK;
+}
+
+int vsg_actor_ann_cb(vsg_actor_t* a, const float* embedding, size_t dims, size_t limit, uint64_t* out_keys,
+                     float* out_distances, vsg_ann_done_fn done, void* ctx) {
+    VSG_RANGE();
+    if (!a || (!embedding && dims) || !out_keys || !out_distances || !done)
+        return actor_fail(VSG_EINVAL, "null argument");
+    // usearch.rs:259-272, checked before the message is queued
+    if (dims == 0) return actor_fail(VSG_EINVAL, "ann: embedding dimensions == 0");
+    if (dims != a->actor->dimensions())
+        return actor_fail(VSG_EINVAL, "ann: wrong embedding dimensions: " + std::to_string(dims) +
+                                          " != " + std::to_string(a->actor->dimensions()));
+    if (limit == 0) return actor_fail(VSG_EINVAL, "ann: limit must be >= 1");
+    return a->actor->ann_cb(embedding, dims, limit, out_keys, out_distances, done, ctx) ? VSG_EINVAL : VSG_OK;
 }
 
 int vsg_actor_count(vsg_actor_t* a, size_t* out) {

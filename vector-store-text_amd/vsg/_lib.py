@@ -117,6 +117,8 @@ class ShardedOptions(C.Structure):
 
 # void (*)(void* ctx, uint64_t key, int status): vsg_actor_add_or_replace_cb completion
 ADD_DONE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_uint64, C.c_int)
+# void (*)(void* ctx, int status, size_t count): vsg_actor_ann_cb completion
+ANN_DONE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_size_t)
 
 
 class ActorCounters(C.Structure):
@@ -195,6 +197,7 @@ def lib() -> C.CDLL:
         "vsg_actor_sharded": (P, [P]),
         "vsg_actor_new_sharded": (C.c_int, [C.POINTER(ActorOptions), u32, P, C.POINTER(P)]),
         "vsg_actor_add_or_replace_cb": (C.c_int, [P, u64, P, sz, ADD_DONE_FN, P]),
+        "vsg_actor_ann_cb": (C.c_int, [P, P, sz, sz, P, P, ANN_DONE_FN, P]),
         "vsg_actor_size": (sz, [P]),
         "vsg_sharded_new": (C.c_int, [C.POINTER(ShardedOptions), C.POINTER(P)]),
         "vsg_sharded_free": (None, [P]),

@@ -11,7 +11,7 @@ STAGE=${1:-all}
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 if [ "$STAGE" = all ] || [ "$STAGE" = tests ]; then
-  timeout -k 10 1000 python3 -u -m pytest ${PYTEST_PATHS:-tests} -m gpu -q -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+  timeout -k 10 1120 python3 -u -m pytest ${PYTEST_PATHS:-tests} -m gpu -q -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
     > gpurun_out/r05_gpu_tests.log 2>&1 || { tail -60 gpurun_out/r05_gpu_tests.log; exit 1; }
   tail -3 gpurun_out/r05_gpu_tests.log
   timeout -k 10 120 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05_smoke.log 2>&1 || exit 1

@@ -1686,6 +1686,11 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // previous search, so searches issued on two streams never overlapped.
 constexpr size_t WS_MAX = 4;
 
+// Stream order covers a workspace's reuse only on one named stream: the null
+// stream and hipStreamPerThread are handles several threads' streams share, so a
+// workspace last used on either always waits for its completion event.
+static bool same_stream(hipStream_t a, hipStream_t b) { return a == b && a != nullptr && a != hipStreamPerThread; }
+
 static int ws_acquire(vsg_index* h, size_t bytes, hipStream_t s, Workspace** out) {
     Workspace* w = nullptr;
     {
@@ -1697,8 +1702,8 @@ static int ws_acquire(vsg_index* h, size_t bytes, hipStream_t s, Workspace** out
         size_t ready = none, fit = none, big = none;
         for (size_t i = 0; i < none; ++i) {
             Workspace* c = h->ws_free[i];
-            if (c->pending && c->last != s && hipEventQuery(c->done) == hipSuccess) c->pending = false;
-            const bool nowait = !c->pending || c->last == s;
+            if (c->pending && !same_stream(c->last, s) && hipEventQuery(c->done) == hipSuccess) c->pending = false;
+            const bool nowait = !c->pending || same_stream(c->last, s);
             if (c->cap >= bytes && nowait && (ready == none || c->cap < h->ws_free[ready]->cap)) ready = i;
             if (c->cap >= bytes && (fit == none || c->cap < h->ws_free[fit]->cap)) fit = i;
             if (big == none || c->cap > h->ws_free[big]->cap) big = i;
@@ -1736,7 +1741,7 @@ static int ws_acquire(vsg_index* h, size_t bytes, hipStream_t s, Workspace** out
             return fail(VSG_ENOMEM, "search workspace");
         }
         w->cap = want;
-    } else if (w->pending && w->last != s) {
+    } else if (w->pending && !same_stream(w->last, s)) {
         const hipError_t e = hipStreamWaitEvent(s, w->done, 0);
         if (e != hipSuccess) {
             std::lock_guard<std::mutex> lk(h->ctx_mu);

@@ -578,6 +578,37 @@ static void test_read_workers_overlap() {
     }
 }
 
+// 6) replace segments: a run of replaces is applied in segments of at most
+//    live / replace_div removes (each followed by its adds), so a re-linked key
+//    sees all but a small fraction of the index live, as the reference's
+//    one-message-at-a-time replace does; the final state is the sequential one
+static void test_replace_segments() {
+    std::vector<Call> log;
+    std::vector<size_t> res;
+    auto* m = new Mock(2, 8, &log, &res, 0);
+    Mock* mp = m;
+    vsg::ActorConfig cfg;
+    cfg.reserve_increment = 4096;
+    vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), cfg);
+    CHECK(a.init() == 0);
+    float v[2] = {1.f, 2.f};
+    for (uint64_t k = 0; k < 640; ++k) a.add_or_replace(k, v);
+    CHECK(a.flush() == 0);
+    log.clear();
+    float w[2] = {3.f, 4.f};
+    for (uint64_t k = 0; k < 100; ++k) a.add_or_replace(k, w);
+    CHECK(a.flush() == 0);
+    size_t removes = 0, removed = 0;
+    for (const Call& c : log)
+        if (c.op == 'r') {
+            ++removes;
+            removed += c.n;
+            CHECK(c.n <= 640 / 64);
+        }
+    CHECK(removed == 100 && removes >= 10);
+    CHECK(mp->rows.size() == 640 && mp->rows[5][0] == 3.f && mp->rows[300][0] == 1.f);
+}
+
 int main() {
     test_concurrent_reads_beside_writes();
     test_read_workers_overlap();
@@ -588,6 +619,7 @@ int main() {
     test_add_errors_swallowed();
     test_add_completions();
     test_auto_compaction();
+    test_replace_segments();
     std::printf("ok\n");
     return 0;
 }

@@ -8,6 +8,7 @@ lock, so a search issued during a 900k-row build answers at once.  Its results c
 a prefix of the writes: every returned key is a key already added or being added, with
 its exact distance (rows are written before any link to them), ascending.
 """
+import gc
 import threading
 import time
 
@@ -43,6 +44,12 @@ def test_search_during_a_large_add():
     torch.cuda.synchronize()
     done = threading.Event()
     t_add = {}
+    # An index of an earlier test left in a reference cycle would be freed by a garbage
+    # collection this loop triggers: vsg_index_free's hipFree waits for the whole device,
+    # i.e. for this build (a 361 ms "search" in the full suite).  Collect first, then hold
+    # collections off while the build runs.
+    gc.collect()
+    gc.disable()
 
     def writer():
         t0 = time.perf_counter()
@@ -65,6 +72,7 @@ def test_search_during_a_large_add():
             if dt > 0.02:
                 slow.append((round(t0 - t_start, 3), round(dt, 3)))
     th.join()
+    gc.enable()
     print("slow searches (start s, latency s):", slow)
     xh = xt.cpu().numpy()
     print(f"add {t_add['s']:.3f} s; {len(lat)} searches during it, max latency {max(lat or [0]) * 1e3:.1f} ms")

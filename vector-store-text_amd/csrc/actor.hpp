@@ -83,6 +83,17 @@ struct ActorConfig {
     // are in flight at once (the GPU overlaps one batch's tail with the next,
     // DESIGN.md §3.2); at most 8
     uint32_t concurrent_reads = 0;
+    // A write segment applies all its removes, then all its adds.  The reference
+    // applies each replace as remove + add before the next message (usearch.rs:
+    // 214-221), so the key re-linked into a freed slot still sees every later key of
+    // the stream live.  Batching R replaces removes R rows at once, and the first of
+    // them are re-linked while the others are tombstones that may not be admitted as
+    // neighbours: self-recall after whole-index replace rounds drops from 0.999
+    // (sequential) to 0.98 at R = 256 and 0.87 at R = 3,000 of 3,000 keys (oracle,
+    // DESIGN.md §3.3a).  A segment therefore closes after live / replace_div removes
+    // (>= 1): at most 1/64 of the index is between its remove and its re-add
+    // (0: unbounded, round 5's first form; VSG_ACTOR_REPLACE_DIV overrides, probes).
+    size_t replace_div = 64;
 };
 
 struct ActorCounters {
@@ -357,9 +368,13 @@ class Actor {
             std::lock_guard<std::mutex> lk(cm_);
             ctr_.writes += i1 - i0;
         }
+        size_t rm_cap = replace_cap();
         for (size_t i = i0; i < i1; ++i) {
             const Msg& m = b[i];
-            if (s.touched.count(m.key)) apply(s);
+            if (s.touched.count(m.key) || s.rm.size() >= rm_cap) {
+                apply(s);
+                rm_cap = replace_cap();
+            }
             s.touched.insert(m.key);
             if (m.kind == REMOVE) {
                 s.rm.push_back(m.key);
@@ -371,6 +386,10 @@ class Actor {
             }
         }
         apply(s);
+    }
+
+    size_t replace_cap() const {  // replace_div 0: unbounded segments (probes)
+        return cfg_.replace_div ? std::max<size_t>(1, be_->size() / cfg_.replace_div) : SIZE_MAX;
     }
 
     void apply(WriteSeg& s) {

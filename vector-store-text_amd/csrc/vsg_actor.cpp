@@ -86,6 +86,7 @@ vsg::ActorConfig actor_config(const vsg_actor_options_t* o) {
     if (o->compact_percent) cfg.compact_percent = o->compact_percent;  // 0 => never (vsg.h)
     if (o->compact_min_dead) cfg.compact_min_dead = o->compact_min_dead;
     cfg.concurrent_reads = o->concurrent_reads;  // 0, 1, or n read workers (capped at 8)
+    if (const char* e = std::getenv("VSG_ACTOR_REPLACE_DIV")) cfg.replace_div = std::strtoull(e, nullptr, 10);
     return cfg;
 }
 

@@ -995,8 +995,15 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
     const double frac = env_double("VSG_BUILD_BATCH_FRAC2", 0.5);
     const double switch_at = env_double("VSG_BUILD_BATCH_SWITCH", 8192);
     const size_t bmax = (size_t)env_double("VSG_BUILD_BATCH_MAX", 65536);
-    // at least 8 batches per call, so the call's own nodes find each other
-    const size_t bcall = std::max<size_t>(1, n / std::max<size_t>(1, (size_t)env_double("VSG_BUILD_MIN_BATCHES", 8)));
+    // at least 8 batches per call, so the call's own nodes find each other; 32 under
+    // inner product, whose graph loses more to batch-mates that cannot link: C5's 200k
+    // x 1536 IP rows, recall@10 at ef 24 (oracle's build 0.9864): 8 batches-min 0.9732,
+    // 16 0.9809, 24 0.9828, 32 0.9841; at 1M rows the 65,536 cap binds first and 32
+    // changes nothing (0.9364 vs 0.9324, +3 % time); cos C2 loses nothing at 8
+    // (profiles/r05_c5_sched.jsonl, r05_minb.jsonl)
+    const double minb_default = h->mk == MK_DOT && !h->normalize ? 32 : 8;
+    const size_t bcall =
+        std::max<size_t>(1, n / std::max<size_t>(1, (size_t)env_double("VSG_BUILD_MIN_BATCHES", minb_default)));
     // re-link pass (reused slots): a batch's reused nodes see each other's cleared
     // rows (dead ends) where the sequential update would see their new links, so the
     // pass takes smaller batches -- at most graph / VSG_REUSE_BATCH_DIV nodes
@@ -2028,9 +2035,12 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         // VSG_SEARCH_REG=0 selects the LDS-list kernels
         p.reg = env_double("VSG_SEARCH_REG", 1) != 0 ? 1 : 0;
         p.upper_ef = upper_ef;
-        // persistent grid of resident waves (register kernel): measured +4-7 % at C2
-        // (profiles/r05_persist.jsonl); VSG_SEARCH_PERSIST=0: one workgroup per query
-        if (env_double("VSG_SEARCH_PERSIST", 1) != 0) p.qnext = qnext;
+        // persistent grid of resident waves (register kernel), for rows >= 1 KiB: C2
+        // (3 KiB rows, HBM-bound) +4-7 % (profiles/r05_persist.jsonl); a C4 shard
+        // (256 B rows, latency-bound) needs every resident wave: half of them cost
+        // 37 % at ef 192 and all of them gain nothing over the plain grid
+        // (r05_c4_persist.jsonl, r05_c4_pfrac.jsonl).  VSG_SEARCH_PERSIST=0 / 1 forces
+        if (env_double("VSG_SEARCH_PERSIST", h->row_bytes >= 1024 ? 1 : 0) != 0) p.qnext = qnext;
         // removed entries among the published slots (tombstones, rolled-back
         // adds): usearch's `allow` predicate -- traversed, never results
         if (filt) {

@@ -673,3 +673,28 @@ def test_exact_only_ktile_mfma_bitexact(metric, dim, monkeypatch):
     check()
     assert idx.compact() == len(keys[::9])   # rows move: the copy is rebuilt by the next search
     check()
+
+
+def test_exact_only_ktile_copy_failure_keeps_the_add(monkeypatch):
+    """the K-tiled copy failing after a successful build must not
+    turn a committed add into a reported failure.  The add returns OK with its rows
+    live and counted (stats.ktile_copy_failures); an exact search while the copy still
+    fails reports the error instead of reading a stale copy; once it can be made, the
+    next exact search finishes the copy and answers exactly."""
+    dim = 64
+    x = G.uint8_valued(1200, dim, 311)
+    q = G.uint8_valued(40, dim, 312)
+    idx = vsg.Index(dim, "l2sq", exact_only=True)
+    idx.add(np.arange(600, dtype=np.uint64), x[:600])
+    idx.exact_search(q, 10)  # the copy exists and is current
+    monkeypatch.setenv("VSG_TEST_FAIL_KTILE", "1")
+    idx.add(np.arange(600, 1200, dtype=np.uint64), x[600:])  # no exception: the add is committed
+    assert idx.size() == 1200 and all(idx.contains(k) for k in (600, 900, 1199))
+    assert idx.stats()["ktile_copy_failures"] >= 1
+    with pytest.raises(vsg.VsgError):
+        idx.exact_search(q, 10)
+    monkeypatch.delenv("VSG_TEST_FAIL_KTILE")
+    ok, od, oc = O.exact_search("l2sq", x, q, 10)
+    m = idx.exact_search(q, 10)
+    np.testing.assert_array_equal(m.keys, ok)
+    np.testing.assert_array_equal(m.distances, od)

@@ -70,12 +70,23 @@ inline void dispatch_shape(int nc, F&& f) {
 // profiles/r03_c4_shape_probe.jsonl).  The build keeps 16 x 1 (8 x 2: +9 % build
 // time, more selection rows per pass).  Distances are the same sums in another lane
 // order: exact on integer data, within rounding otherwise.
+//
+// 129..192-chunk rows (768-d f32 -- C2, C3) search with 4 passes in flight instead of
+// the build's 2: a query's chain is ~22 expansions of ~30 fresh 3-KiB rows, and one
+// wave with 4 rows in flight needs half the round trips per expansion.  Kernel ms at
+// C2, ef 36, U 2 -> 4 (profiles/r05_shape_u4.jsonl): 512 queries 0.593 -> 0.509,
+// 2,048 0.923 -> 0.854, 10,000 2.993 -> 2.998 -- small batches (the actor's) gain,
+// the full chip does not lose.  Same sums in the same order: identical results.
 #ifndef VSG_SEARCH_SHAPE16
 #define VSG_SEARCH_SHAPE16 8, 2, 4
+#endif
+#ifndef VSG_SEARCH_SHAPE192
+#define VSG_SEARCH_SHAPE192 32, 6, 4
 #endif
 template <typename F>
 inline void dispatch_shape_search(int nc, F&& f) {
     if (nc > 4 && nc <= 16) f(Shape<VSG_SEARCH_SHAPE16>{});
+    else if (nc > 128 && nc <= 192) f(Shape<VSG_SEARCH_SHAPE192>{});
     else dispatch_shape(nc, f);
 }
 

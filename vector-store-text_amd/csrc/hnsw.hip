@@ -1034,7 +1034,7 @@ hipError_t launch_edge_dist_refresh(Storage st, MetricKind mk, const DevGraph& g
     if (!g.adjd0) return hipErrorInvalidValue;
     hipError_t err = hipSuccess;
     const unsigned grid = (unsigned)std::min<size_t>(n, 1u << 20);
-    dispatch_all(st, mk, g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<SHAPE_BUILD>(st, mk, g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(edge_dist_refresh_kernel, sh, tt, mt);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, s, g, levels, flags, (uint32_t)n);
         err = hipGetLastError();
@@ -1050,7 +1050,7 @@ hipError_t launch_edge_dist_fill(Storage st, MetricKind mk, const DevGraph& g, c
     // upper rows (a small loaded / imported index) has none to fill
     if (!g.adjd0) return hipErrorInvalidValue;
     hipError_t err = hipSuccess;
-    dispatch_all(st, mk, g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<SHAPE_BUILD>(st, mk, g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(edge_dist_fill_kernel, sh, tt, mt);
         hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(64), 0, s, g, levels, (uint32_t)n);
         err = hipGetLastError();
@@ -1074,7 +1074,7 @@ hipError_t launch_search(Storage st, MetricKind mk, const SearchParams& p, hipSt
     const int nw = (p.waves == 2 || p.waves == 4) && p.g.M0 <= 64 ? p.waves : 1;
     const size_t lds = search_lds_bytes(p.ef, p.hash_size, nw);
     hipError_t err = hipSuccess;
-    dispatch_all<true>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<SHAPE_SEARCH>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto run = [&](auto kern) {
             if (lds > 65536)
                 (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1105,7 +1105,7 @@ hipError_t launch_insert(Storage st, MetricKind mk, const InsertParams& p, hipSt
     if (p.nnodes <= 0) return hipSuccess;
     const size_t lds = insert_lds_bytes(p.efc, p.hash_size, p.g.M0);
     hipError_t err = hipSuccess;
-    dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<SHAPE_BUILD>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(hnsw_insert_kernel, sh, tt, mt);
         if (lds > 65536) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3(p.nnodes), dim3(64), lds, s, p);
@@ -1120,7 +1120,7 @@ hipError_t launch_insert_split(Storage st, MetricKind mk, const InsertParams& p,
     const size_t lds_beam = wave_lds_bytes(p.hash_size, p.efc, 0);
     const size_t lds_sel = wave_lds_bytes(0, p.efc, sel_entries(p.g.M0));
     hipError_t err = hipSuccess;
-    dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<SHAPE_BUILD>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kb = VSG_KERNEL_OF(hnsw_insert_beam_kernel, sh, tt, mt);
         auto ks = VSG_KERNEL_OF(hnsw_insert_select_kernel, sh, tt, mt);
         if (lds_beam > 65536) (void)hipFuncSetAttribute((const void*)kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_beam);
@@ -1140,7 +1140,7 @@ hipError_t launch_reverse(Storage st, MetricKind mk, const ReverseParams& p, int
     const int cap = 2 * p.g.M0 > 64 ? 2 * p.g.M0 : 64;
     const size_t lds = insert_lds_bytes(cap, 0, p.g.M0);
     hipError_t err = hipSuccess;
-    dispatch_all(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<SHAPE_BUILD>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         auto kern = VSG_KERNEL_OF(hnsw_reverse_kernel, sh, tt, mt);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, p);
         err = hipGetLastError();

@@ -393,7 +393,7 @@ static hipError_t launch_filt_rerun(Storage st, MetricKind mk, const SearchParam
     r.hash_size = std::max(1024, std::min(p.hash_size, 16384));
     const size_t lds = search_reg_lds_bytes(r.hash_size);
     hipError_t err = hipSuccess;
-    dispatch_all<true>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<SHAPE_SEARCH>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
         using T = typename decltype(tt)::T;
         constexpr int MET = decltype(mt)::MET;
@@ -454,8 +454,8 @@ hipError_t launch_search_filt(Storage st, MetricKind mk, const SearchParams& p, 
             else if (rows == 8) run(hnsw_search_reg_filt_kernel<G, VM, U, T, MET, 8>);
             else run(hnsw_search_reg_filt_kernel<G, VM, U, T, MET, 17>);
         };
-        if (rows == 17) dispatch_all<false>(st, mk, p.g.nchunks, body);
-        else dispatch_all<true>(st, mk, p.g.nchunks, body);
+        if (rows == 17) dispatch_all<SHAPE_GENERIC>(st, mk, p.g.nchunks, body);
+        else dispatch_all<SHAPE_SEARCH>(st, mk, p.g.nchunks, body);
         if (err == hipSuccess) err = launch_filt_rerun(st, mk, p, s);
         return err;
     }
@@ -468,7 +468,7 @@ hipError_t launch_search_filt(Storage st, MetricKind mk, const SearchParams& p, 
     const int hmax = (int)(((160 * 1024) - (size_t)cap * 16 - 64 * 16 - 1024) / 4) & ~63;
     pl.hash_size = std::max(1024, std::min(p.hash_size, hmax));
     const size_t lds = wave_lds_bytes(pl.hash_size, cap, 0);
-    dispatch_all<true>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
+    dispatch_all<SHAPE_SEARCH>(st, mk, p.g.nchunks, [&](auto sh, auto tt, auto mt) {
         constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
         using T = typename decltype(tt)::T;
         constexpr int MET = decltype(mt)::MET;

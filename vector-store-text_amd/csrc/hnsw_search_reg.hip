@@ -231,8 +231,8 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
     };
     // the search row shape (dispatch_shape_search), except with 17 register rows
     // (ef > 448), where the 8 x 2 shape of 64-d f32 rows spills registers
-    if (rows == 17) dispatch_all<false>(st, mk, p.g.nchunks, body);
-    else dispatch_all<true>(st, mk, p.g.nchunks, body);
+    if (rows == 17) dispatch_all<SHAPE_GENERIC>(st, mk, p.g.nchunks, body);
+    else dispatch_all<SHAPE_SEARCH>(st, mk, p.g.nchunks, body);
     return err;
 }
 

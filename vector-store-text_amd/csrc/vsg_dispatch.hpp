@@ -10,7 +10,8 @@
 //   chunks <=  96: G 32, VM 3,  U 4   (D=384 f32, D=768 f16)
 //   chunks <= 128: G 64, VM 2,  U 4
 //   chunks <= 192: G 32, VM 6,  U 2   (D=768 f32; was G 64 VM 3 U 4: search +1.7 %, build +6 %,
-//                                      profiles/r01_shape192_probe.jsonl)
+//                                      profiles/r01_shape192_probe.jsonl; the build and
+//                                      search kernels take U 4, below)
 //   chunks <= 256: G 64, VM 4,  U 2
 //   chunks <= 384: G 64, VM 6,  U 2   (D=1536 f32)
 //   chunks <= 512: G 64, VM 8,  U 2
@@ -71,30 +72,51 @@ inline void dispatch_shape(int nc, F&& f) {
 // time, more selection rows per pass).  Distances are the same sums in another lane
 // order: exact on integer data, within rounding otherwise.
 //
-// 129..192-chunk rows (768-d f32 -- C2, C3) search with 4 passes in flight instead of
-// the build's 2: a query's chain is ~22 expansions of ~30 fresh 3-KiB rows, and one
+// 4 passes in flight for 768-d and 1536-d f32 rows (C2 / C3, C5) in the search kernels
+// (round 5): a query's chain is ~22 expansions of ~30 fresh 3- / 6-KiB rows, and one
 // wave with 4 rows in flight needs half the round trips per expansion.  Kernel ms at
-// C2, ef 36, U 2 -> 4 (profiles/r05_shape_u4.jsonl): 512 queries 0.593 -> 0.509,
-// 2,048 0.923 -> 0.854, 10,000 2.993 -> 2.998 -- small batches (the actor's) gain,
-// the full chip does not lose.  Same sums in the same order: identical results.
+// ef 36 / 30, U 2 -> 4 (profiles/r05_shape_u4.jsonl, r05_c5u4.jsonl): C2 512 queries
+// 0.593 -> 0.509, 2,048 0.923 -> 0.854, 10,000 2.993 -> 2.998; C5 512 0.593 -> 0.500,
+// 10,000 4.237 -> 4.172 -- small batches (the actor's) gain, the full chip does not
+// lose.  Same sums in the same order: identical results.  (The 17-row register kernels,
+// ef > 448, keep dispatch_shape: their key set leaves no room for 4 passes.)
 #ifndef VSG_SEARCH_SHAPE16
 #define VSG_SEARCH_SHAPE16 8, 2, 4
 #endif
 #ifndef VSG_SEARCH_SHAPE192
 #define VSG_SEARCH_SHAPE192 32, 6, 4
 #endif
+#ifndef VSG_SEARCH_SHAPE384
+#define VSG_SEARCH_SHAPE384 64, 6, 4
+#endif
 template <typename F>
 inline void dispatch_shape_search(int nc, F&& f) {
     if (nc > 4 && nc <= 16) f(Shape<VSG_SEARCH_SHAPE16>{});
     else if (nc > 128 && nc <= 192) f(Shape<VSG_SEARCH_SHAPE192>{});
+    else if (nc > 256 && nc <= 384) f(Shape<VSG_SEARCH_SHAPE384>{});
     else dispatch_shape(nc, f);
 }
 
-// f(Shape, TypeTag, MetTag); SEARCH selects dispatch_shape_search
-template <bool SEARCH = false, typename F>
+// The build kernels' shape (insert beam / selection, reverse links, edge distances):
+// 768-d f32 rows with 4 passes in flight too -- C2 build 0.485 -> 0.468 s, insert
+// 0.435 -> 0.418 s, same graph (profiles/r05_b4_build.jsonl).
+#ifndef VSG_BUILD_SHAPE192
+#define VSG_BUILD_SHAPE192 32, 6, 4
+#endif
+template <typename F>
+inline void dispatch_shape_build(int nc, F&& f) {
+    if (nc > 128 && nc <= 192) f(Shape<VSG_BUILD_SHAPE192>{});
+    else dispatch_shape(nc, f);
+}
+
+enum ShapeMode { SHAPE_GENERIC = 0, SHAPE_SEARCH = 1, SHAPE_BUILD = 2 };
+
+// f(Shape, TypeTag, MetTag); MODE selects the search / build shapes
+template <int MODE = SHAPE_GENERIC, typename F>
 inline void dispatch_all(Storage st, MetricKind mk, int nc, F&& f) {
     auto pick = [&](auto&& g) {
-        if constexpr (SEARCH) dispatch_shape_search(nc, g);
+        if constexpr (MODE == SHAPE_SEARCH) dispatch_shape_search(nc, g);
+        else if constexpr (MODE == SHAPE_BUILD) dispatch_shape_build(nc, g);
         else dispatch_shape(nc, g);
     };
     pick([&](auto sh) {

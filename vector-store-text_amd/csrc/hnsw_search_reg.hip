@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <type_traits>
 #include <mutex>
 #include <tuple>
 
@@ -193,46 +194,54 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
         const int r = atoi(e);
         if ((r == 2 || r == 4 || r == 8 || r == 17) && 64 * r >= p.ef + 64) rows = r;
     }
-    auto body = [&](auto sh, auto tt, auto mt) {
-        constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
-        using T = typename decltype(tt)::T;
-        constexpr int MET = decltype(mt)::MET;
-        auto run = [&](auto kern) {
-            if (lds > 65536)
-                (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            constexpr int CH = 1 << 22;  // 64 work-items each: the AQL grid size is 32-bit
-            for (int off = 0; off < p.nq && err == hipSuccess; off += CH) {
-                SearchParams c = p;
-                c.nq = min(CH, p.nq - off);
-                c.queries = p.queries + (size_t)off * p.g.row_bytes;
-                c.out_keys = p.out_keys + (size_t)off * p.k;
-                c.out_dist = p.out_dist + (size_t)off * p.k;
-                c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
-                unsigned grid = (unsigned)c.nq;
-                if (p.qnext) {  // persistent: one round of resident waves, counter reset per launch
-                    // half of the resident waves: at C2 the kernel is throughput-bound from
-                    // ~0.35 of the occupancy on, and fewer waves end the batch sooner (fractions
-                    // 0.25 / 0.35 / 0.5 / 0.6 / 1.0: 3.20 / 3.35 / 3.34 / 3.34 / 3.28 M QPS,
-                    // profiles/r05_pfrac.jsonl); VSG_SEARCH_PERSIST_FRAC overrides (probes)
-                    static const double frac = std::min(1.0, std::max(0.05, env_frac("VSG_SEARCH_PERSIST_FRAC", 0.5)));
-                    const int res = std::max(1, (int)(frac * resident_blocks((const void*)kern, lds)));
-                    grid = (unsigned)std::max(1, std::min(c.nq, res));
-                    err = hipMemsetAsync(p.qnext, 0, sizeof(unsigned), s);
-                    if (err != hipSuccess) break;
+    // R (register rows) fixed at compile time, so each row shape is instantiated only
+    // for the R classes that use it
+    auto launch_rows = [&](auto rtag) {
+        constexpr int R = decltype(rtag)::value;
+        auto body = [&](auto sh, auto tt, auto mt) {
+            constexpr int G = decltype(sh)::G, VM = decltype(sh)::VM, U = decltype(sh)::U;
+            using T = typename decltype(tt)::T;
+            constexpr int MET = decltype(mt)::MET;
+            auto run = [&](auto kern) {
+                if (lds > 65536)
+                    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                constexpr int CH = 1 << 22;  // 64 work-items each: the AQL grid size is 32-bit
+                for (int off = 0; off < p.nq && err == hipSuccess; off += CH) {
+                    SearchParams c = p;
+                    c.nq = min(CH, p.nq - off);
+                    c.queries = p.queries + (size_t)off * p.g.row_bytes;
+                    c.out_keys = p.out_keys + (size_t)off * p.k;
+                    c.out_dist = p.out_dist + (size_t)off * p.k;
+                    c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
+                    unsigned grid = (unsigned)c.nq;
+                    if (p.qnext) {  // persistent: one round of resident waves, counter reset per launch
+                        // half of the resident waves: at C2 the kernel is throughput-bound from
+                        // ~0.35 of the occupancy on, and fewer waves end the batch sooner (fractions
+                        // 0.25 / 0.35 / 0.5 / 0.6 / 1.0: 3.20 / 3.35 / 3.34 / 3.34 / 3.28 M QPS,
+                        // profiles/r05_pfrac.jsonl); VSG_SEARCH_PERSIST_FRAC overrides (probes)
+                        static const double frac = std::min(1.0, std::max(0.05, env_frac("VSG_SEARCH_PERSIST_FRAC", 0.5)));
+                        const int res = std::max(1, (int)(frac * resident_blocks((const void*)kern, lds)));
+                        grid = (unsigned)std::max(1, std::min(c.nq, res));
+                        err = hipMemsetAsync(p.qnext, 0, sizeof(unsigned), s);
+                        if (err != hipSuccess) break;
+                    }
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, c);
+                    err = hipGetLastError();
                 }
-                hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, s, c);
-                err = hipGetLastError();
-            }
+            };
+            run(hnsw_search_reg_kernel<G, VM, U, T, MET, R>);
         };
-        if (rows == 2) run(hnsw_search_reg_kernel<G, VM, U, T, MET, 2>);
-        else if (rows == 4) run(hnsw_search_reg_kernel<G, VM, U, T, MET, 4>);
-        else if (rows == 8) run(hnsw_search_reg_kernel<G, VM, U, T, MET, 8>);
-        else run(hnsw_search_reg_kernel<G, VM, U, T, MET, 17>);
+        // the search row shape (dispatch_shape_search): 4 passes for long rows with 2 register
+        // rows (vsg_dispatch.hpp); with 17 (ef > 448) the generic shape, where the 8 x 2 shape
+        // of 64-d f32 rows spills registers
+        if constexpr (R == 17) dispatch_all<SHAPE_GENERIC>(st, mk, p.g.nchunks, body);
+        else if constexpr (R == 2) dispatch_all<SHAPE_SEARCH_SMALL_EF>(st, mk, p.g.nchunks, body);
+        else dispatch_all<SHAPE_SEARCH>(st, mk, p.g.nchunks, body);
     };
-    // the search row shape (dispatch_shape_search), except with 17 register rows
-    // (ef > 448), where the 8 x 2 shape of 64-d f32 rows spills registers
-    if (rows == 17) dispatch_all<SHAPE_GENERIC>(st, mk, p.g.nchunks, body);
-    else dispatch_all<SHAPE_SEARCH>(st, mk, p.g.nchunks, body);
+    if (rows == 2) launch_rows(std::integral_constant<int, 2>{});
+    else if (rows == 4) launch_rows(std::integral_constant<int, 4>{});
+    else if (rows == 8) launch_rows(std::integral_constant<int, 8>{});
+    else launch_rows(std::integral_constant<int, 17>{});
     return err;
 }
 

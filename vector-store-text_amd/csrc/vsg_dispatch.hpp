@@ -73,13 +73,15 @@ inline void dispatch_shape(int nc, F&& f) {
 // order: exact on integer data, within rounding otherwise.
 //
 // 4 passes in flight for 768-d and 1536-d f32 rows (C2 / C3, C5) in the search kernels
-// (round 5): a query's chain is ~22 expansions of ~30 fresh 3- / 6-KiB rows, and one
+// at ef <= 64 (round 5): a query's chain is ~22 expansions of ~30 fresh 3- / 6-KiB rows, and one
 // wave with 4 rows in flight needs half the round trips per expansion.  Kernel ms at
 // ef 36 / 30, U 2 -> 4 (profiles/r05_shape_u4.jsonl, r05_c5u4.jsonl): C2 512 queries
 // 0.593 -> 0.509, 2,048 0.923 -> 0.854, 10,000 2.993 -> 2.998; C5 512 0.593 -> 0.500,
 // 10,000 4.237 -> 4.172 -- small batches (the actor's) gain, the full chip does not
-// lose.  Same sums in the same order: identical results.  (The 17-row register kernels,
-// ef > 448, keep dispatch_shape: their key set leaves no room for 4 passes.)
+// lose.  Same sums in the same order: identical results.  Only the 2-row register
+// kernels (ef <= 64) take it: with 4 register rows the extra VGPRs cost a wave per SIMD,
+// C2 at ef 128 1.83 -> 1.70 M QPS; the list kernels and the 17-row register kernels
+// (ef > 448, whose key set leaves no room) keep U=2.
 #ifndef VSG_SEARCH_SHAPE16
 #define VSG_SEARCH_SHAPE16 8, 2, 4
 #endif
@@ -89,11 +91,11 @@ inline void dispatch_shape(int nc, F&& f) {
 #ifndef VSG_SEARCH_SHAPE384
 #define VSG_SEARCH_SHAPE384 64, 6, 4
 #endif
-template <typename F>
+template <bool LONG_U4, typename F>
 inline void dispatch_shape_search(int nc, F&& f) {
     if (nc > 4 && nc <= 16) f(Shape<VSG_SEARCH_SHAPE16>{});
-    else if (nc > 128 && nc <= 192) f(Shape<VSG_SEARCH_SHAPE192>{});
-    else if (nc > 256 && nc <= 384) f(Shape<VSG_SEARCH_SHAPE384>{});
+    else if (LONG_U4 && nc > 128 && nc <= 192) f(Shape<VSG_SEARCH_SHAPE192>{});
+    else if (LONG_U4 && nc > 256 && nc <= 384) f(Shape<VSG_SEARCH_SHAPE384>{});
     else dispatch_shape(nc, f);
 }
 
@@ -109,13 +111,15 @@ inline void dispatch_shape_build(int nc, F&& f) {
     else dispatch_shape(nc, f);
 }
 
-enum ShapeMode { SHAPE_GENERIC = 0, SHAPE_SEARCH = 1, SHAPE_BUILD = 2 };
+// SHAPE_SEARCH_SMALL_EF: the 2-row register search kernels (long rows with U=4)
+enum ShapeMode { SHAPE_GENERIC = 0, SHAPE_SEARCH = 1, SHAPE_BUILD = 2, SHAPE_SEARCH_SMALL_EF = 3 };
 
 // f(Shape, TypeTag, MetTag); MODE selects the search / build shapes
 template <int MODE = SHAPE_GENERIC, typename F>
 inline void dispatch_all(Storage st, MetricKind mk, int nc, F&& f) {
     auto pick = [&](auto&& g) {
-        if constexpr (MODE == SHAPE_SEARCH) dispatch_shape_search(nc, g);
+        if constexpr (MODE == SHAPE_SEARCH) dispatch_shape_search<false>(nc, g);
+        else if constexpr (MODE == SHAPE_SEARCH_SMALL_EF) dispatch_shape_search<true>(nc, g);
         else if constexpr (MODE == SHAPE_BUILD) dispatch_shape_build(nc, g);
         else dispatch_shape(nc, g);
     };

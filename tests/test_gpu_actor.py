@@ -206,7 +206,9 @@ def test_actor_upsert_stream_reuses_slots():
     _, d_o, _ = h_o.search(mat, 1, 64, threads=8)
     ref = float(np.mean(d_o[:, 0] == 0.0))
     print(f"oracle, one replace at a time: self-hit {ref:.4f}")
-    _self_hits(a, mat, ref - 0.01)
+    # the actor's segments follow its drain timing (round 0's batched appends too): 0.983 -
+    # 0.995 over runs; unbounded segments gave 0.889
+    _self_hits(a, mat, ref - 0.02)
     a.close()
 
 

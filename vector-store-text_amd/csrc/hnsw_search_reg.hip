@@ -215,11 +215,13 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
                     c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
                     unsigned grid = (unsigned)c.nq;
                     if (p.qnext) {  // persistent: one round of resident waves, counter reset per launch
-                        // half of the resident waves: at C2 the kernel is throughput-bound from
-                        // ~0.35 of the occupancy on, and fewer waves end the batch sooner (fractions
-                        // 0.25 / 0.35 / 0.5 / 0.6 / 1.0: 3.20 / 3.35 / 3.34 / 3.34 / 3.28 M QPS,
-                        // profiles/r05_pfrac.jsonl); VSG_SEARCH_PERSIST_FRAC overrides (probes)
-                        static const double frac = std::min(1.0, std::max(0.05, env_frac("VSG_SEARCH_PERSIST_FRAC", 0.5)));
+                        // 3/4 of the resident waves: the kernel is throughput-bound below full
+                        // occupancy, and fewer waves end the batch sooner.  C2 fractions 0.35 /
+                        // 0.5 / 0.75 / 1.0 with the U=4 row shape (2 waves/SIMD resident): 3.01 /
+                        // 3.34 / 3.40 / 3.38 M QPS (profiles/r05_pfrac_u4.jsonl); with U=2 (4
+                        // waves/SIMD) 0.35-0.6 were level at 3.34 M (r05_pfrac.jsonl);
+                        // VSG_SEARCH_PERSIST_FRAC overrides (probes)
+                        static const double frac = std::min(1.0, std::max(0.05, env_frac("VSG_SEARCH_PERSIST_FRAC", 0.75)));
                         const int res = std::max(1, (int)(frac * resident_blocks((const void*)kern, lds)));
                         grid = (unsigned)std::max(1, std::min(c.nq, res));
                         err = hipMemsetAsync(p.qnext, 0, sizeof(unsigned), s);

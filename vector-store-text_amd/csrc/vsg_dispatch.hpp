@@ -100,14 +100,19 @@ inline void dispatch_shape_search(int nc, F&& f) {
 }
 
 // The build kernels' shape (insert beam / selection, reverse links, edge distances):
-// 768-d f32 rows with 4 passes in flight too -- C2 build 0.485 -> 0.468 s, insert
-// 0.435 -> 0.418 s, same graph (profiles/r05_b4_build.jsonl).
+// 768-d and 1536-d f32 rows with 4 passes in flight too -- C2 build 0.485 -> 0.468 s
+// (insert 0.435 -> 0.418 s), C5 1M x 1536 IP 1.04 -> 0.985 s (insert 0.971 -> 0.913 s),
+// same graphs (profiles/r05_b4_build.jsonl, r05_c5b4_build.jsonl).
 #ifndef VSG_BUILD_SHAPE192
 #define VSG_BUILD_SHAPE192 32, 6, 4
+#endif
+#ifndef VSG_BUILD_SHAPE384
+#define VSG_BUILD_SHAPE384 64, 6, 4
 #endif
 template <typename F>
 inline void dispatch_shape_build(int nc, F&& f) {
     if (nc > 128 && nc <= 192) f(Shape<VSG_BUILD_SHAPE192>{});
+    else if (nc > 256 && nc <= 384) f(Shape<VSG_BUILD_SHAPE384>{});
     else dispatch_shape(nc, f);
 }
 

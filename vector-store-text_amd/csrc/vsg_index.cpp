@@ -2188,26 +2188,56 @@ static hipError_t copy_chunked(void* dst, const void* src, size_t bytes, hipMemc
     return hipSuccess;
 }
 
-// Host rows -> pinned staging -> device, pipelined: each 16 MiB piece is copied into
-// the pinned buffer by the host threads and its DMA queued at once, so the copy of the
-// next piece overlaps the transfer of this one.  A 10k-query C2 batch is 30 MB: one
-// serial memcpy took ~3 ms before its DMA could start, as long as the search itself.
-// Below 8 MiB (the actor's batches) one memcpy and one transfer.
+// Host rows -> pinned staging -> device, pipelined: T host threads copy the rows into
+// the pinned buffer piece by piece (4 MiB pieces, each thread its slice of every piece,
+// in piece order) while this thread queues each piece's DMA as soon as every slice of it
+// is in, so the transfer of piece p overlaps the copy of the pieces after it.  A
+// 10k-query C2 batch is 30 MB: one serial memcpy took ~3 ms before its DMA could start,
+// as long as the search itself; 16 MiB pieces each copied by freshly started threads
+// still spent 1.35 ms in the upload (profiles/r05_host_search.jsonl).  Below 8 MiB (the
+// actor's batches) one memcpy and one transfer.
 static hipError_t h2d_staged(void* dst, uint8_t* pin, const void* src, size_t bytes, hipStream_t s) {
     if (bytes < ((size_t)8 << 20)) {
         std::memcpy(pin, src, bytes);
         return copy_chunked(dst, pin, bytes, hipMemcpyHostToDevice, s);
     }
-    const size_t CH = (size_t)16 << 20;
-    for (size_t off = 0; off < bytes; off += CH) {
-        const size_t n = std::min(CH, bytes - off);
-        uint8_t* p = pin + off;
-        const uint8_t* q = static_cast<const uint8_t*>(src) + off;
-        host_parallel(n, [&](size_t lo, size_t hi) { std::memcpy(p + lo, q + lo, hi - lo); });
-        const hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, p, n, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) return e;
+    const size_t CH = (size_t)4 << 20;
+    const size_t P = (bytes + CH - 1) / CH;
+    const size_t T = std::min<size_t>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()));
+    std::vector<std::atomic<uint32_t>> done(P);
+    for (auto& d : done) d.store(0, std::memory_order_relaxed);
+    const uint8_t* q = static_cast<const uint8_t*>(src);
+    auto worker = [&](size_t t) {
+        for (size_t p = 0; p < P; ++p) {
+            const size_t off = p * CH, n = std::min(CH, bytes - off);
+            const size_t lo = n * t / T, hi = n * (t + 1) / T;
+            std::memcpy(pin + off + lo, q + off + lo, hi - lo);
+            done[p].fetch_add(1, std::memory_order_release);
+        }
+    };
+    std::vector<std::thread> th;
+    size_t started = 0;
+    try {  // a thread that cannot be started must not throw across the C ABI
+        for (; started < T - 1; ++started) th.emplace_back(worker, started);
+    } catch (const std::system_error&) {
     }
-    return hipSuccess;
+    hipError_t e = hipSuccess;
+    if (started < T - 1) {  // not all threads: copy everything here, then transfer
+        for (auto& t : th) t.join();
+        std::memcpy(pin, src, bytes);
+        return copy_chunked(dst, pin, bytes, hipMemcpyHostToDevice, s);
+    }
+    // this thread takes the last slice of every piece, then queues the piece
+    for (size_t p = 0; p < P; ++p) {
+        const size_t off = p * CH, n = std::min(CH, bytes - off);
+        const size_t lo = n * (T - 1) / T;
+        std::memcpy(pin + off + lo, q + off + lo, n - lo);
+        done[p].fetch_add(1, std::memory_order_release);
+        while (done[p].load(std::memory_order_acquire) < T) std::this_thread::yield();
+        if (e == hipSuccess) e = hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, pin + off, n, hipMemcpyHostToDevice, s);
+    }
+    for (auto& t : th) t.join();
+    return e;
 }
 
 static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,

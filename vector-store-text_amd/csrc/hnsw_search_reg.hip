@@ -129,21 +129,30 @@ __device__ __forceinline__ void search_reg_one(const SearchParams& p, int qi, ui
     }
 }
 
+// Persistent grid only in the instances for rows of >= 1 KiB (the shape's row span,
+// 16-B chunks): compiled into the short-row kernels, the loop's second copy of the
+// search cost the C4 shard kernel 15 VGPRs (87 -> 102: 5 -> 4 waves per SIMD, 2.97 ->
+// 3.23 ms at ef 192) although it never ran there.  launch_search_reg sizes the grid by
+// the same constant.
+template <int G, int VM> constexpr bool persist_shape() { return G * VM * 16 >= 1024; }
+
 template <int G, int VM, int U, typename T, int MET, int R>
 __global__ __launch_bounds__(64) VSG_SEARCH_ATTR void hnsw_search_reg_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if (p.qnext) {
-        // persistent grid (VSG_SEARCH_PERSIST, probes): resident waves take query
-        // indices from a counter until the batch is done
-        for (;;) {
-            int qi = 0;
-            if (lane_id() == 0) qi = (int)atomicAdd(p.qnext, 1u);
-            qi = __builtin_amdgcn_readfirstlane(qi);
-            if (qi >= p.nq) break;
-            search_reg_one<G, VM, U, T, MET, R>(p, qi, smem);
-            wave_sync();
+    if constexpr (persist_shape<G, VM>()) {
+        if (p.qnext) {
+            // persistent grid: resident waves take query indices from a counter until
+            // the batch is done
+            for (;;) {
+                int qi = 0;
+                if (lane_id() == 0) qi = (int)atomicAdd(p.qnext, 1u);
+                qi = __builtin_amdgcn_readfirstlane(qi);
+                if (qi >= p.nq) break;
+                search_reg_one<G, VM, U, T, MET, R>(p, qi, smem);
+                wave_sync();
+            }
+            return;
         }
-        return;
     }
     int qi = blockIdx.x;
     if (p.xcd_map) {
@@ -214,7 +223,7 @@ hipError_t launch_search_reg(Storage st, MetricKind mk, const SearchParams& p, h
                     c.out_dist = p.out_dist + (size_t)off * p.k;
                     c.out_counts = p.out_counts ? p.out_counts + off : nullptr;
                     unsigned grid = (unsigned)c.nq;
-                    if (p.qnext) {  // persistent: one round of resident waves, counter reset per launch
+                    if (persist_shape<G, VM>() && p.qnext) {  // persistent: one round of resident waves, counter reset per launch
                         // 3/4 of the resident waves: the kernel is throughput-bound below full
                         // occupancy, and fewer waves end the batch sooner.  C2 fractions 0.35 /
                         // 0.5 / 0.75 / 1.0 with the U=4 row shape (2 waves/SIMD resident): 3.01 /

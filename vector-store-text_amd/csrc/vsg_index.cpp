@@ -2039,7 +2039,8 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         // (3 KiB rows, HBM-bound) +4-7 % (profiles/r05_persist.jsonl); a C4 shard
         // (256 B rows, latency-bound) needs every resident wave: half of them cost
         // 37 % at ef 192 and all of them gain nothing over the plain grid
-        // (r05_c4_persist.jsonl, r05_c4_pfrac.jsonl).  VSG_SEARCH_PERSIST=0 / 1 forces
+        // (r05_c4_persist.jsonl, r05_c4_pfrac.jsonl).  VSG_SEARCH_PERSIST=0 / 1 forces (the
+        // short-row kernels are compiled without the loop: hnsw_search_reg.hip persist_shape)
         if (env_double("VSG_SEARCH_PERSIST", h->row_bytes >= 1024 ? 1 : 0) != 0) p.qnext = qnext;
         // removed entries among the published slots (tombstones, rolled-back
         // adds): usearch's `allow` predicate -- traversed, never results

@@ -19,17 +19,31 @@ os.makedirs(dst, exist_ok=True)
 stats = glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True)
 trace = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)
 lines = [f"# rocprofv3 kernel summary — {tag}", ""]
+
+
+def demangle(name):
+    """Some rocprofv3 runs report mangled kernel names (_ZN3vsg...): demangle with c++filt."""
+    if not name.startswith("_Z"):
+        return name
+    try:
+        import subprocess
+        out = subprocess.run(["c++filt", name], capture_output=True, text=True, timeout=10).stdout.strip()
+        return out or name
+    except Exception:  # noqa: BLE001 -- keep the raw name
+        return name
+
+
 if stats:
     shutil.copy(stats[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats[0])))
     lines += ["| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
     for r in rows[:12]:
-        lines.append(f"| `{r['Name'][:80]}` | {r['Calls']} | {int(r['TotalDurationNs'])/1e6:.2f} | "
+        lines.append(f"| `{demangle(r['Name'])[:80]}` | {r['Calls']} | {int(r['TotalDurationNs'])/1e6:.2f} | "
                      f"{float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.2f} |")
 if trace:
     per = defaultdict(list)
     for r in csv.DictReader(open(trace[0])):
-        name = r["Kernel_Name"]
+        name = demangle(r["Kernel_Name"])
         if "vsg::" not in name or not any(s in name for s in ("hnsw_", "exact", "mfma", "merge")):
             continue
         short = name.split("(")[0].replace("void ", "")

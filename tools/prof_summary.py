@@ -27,8 +27,10 @@ def demangle(name):
         return name
     try:
         import subprocess
-        out = subprocess.run(["c++filt", name], capture_output=True, text=True, timeout=10).stdout.strip()
-        return out or name
+        # GNU c++filt does not know DF16_ (_Float16): demangle it as Dh (half), rename after
+        out = subprocess.run(["c++filt", name.replace("DF16_", "Dh")], capture_output=True, text=True,
+                             timeout=10).stdout.strip()
+        return out.replace("half", "_Float16") if out and not out.startswith("_Z") else name
     except Exception:  # noqa: BLE001 -- keep the raw name
         return name
 

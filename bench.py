@@ -98,6 +98,9 @@ def parse():
                          "devices in rank 0's process (include/vsg.h vsg_sharded_*), peer-DMA gather + HIP merge")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse several ranks on one GPU (collectives via host)")
+    ap.add_argument("--actor-leg", type=int, default=1,
+                    help="N=1: closed-loop single-query anns through the actor (tools/actor_load child "
+                         "process) at 512 and 2,048 clients on the headline index and ef")
     ap.add_argument("--host-abi-leg", type=int, default=1,
                     help="N=1: also time the drop-in's host-buffer ABI -- build via vsg_index_add from host f32 "
                          "rows, QPS via vsg_index_search from host queries (PCIe included) -- beside `value`")
@@ -138,6 +141,40 @@ class Ctx:
         if self.world > 1:
             self.dist.barrier()
         self.torch.cuda.synchronize()
+
+    def rank_devices(self) -> dict:
+        """Which device every rank ran on: each rank's ordinal,
+        PCI address and uuid, all-gathered; the communicator's size, and under RCCL an
+        all-reduce of ones over it (the number of ranks the collective really joined).
+        A duplicated or missing device under RCCL fails the run before any value is
+        printed; the gloo rehearsal on one GPU is flagged as such."""
+        torch, dist = self.torch, self.dist
+        p = torch.cuda.get_device_properties(self.dev)
+        me = {"rank": self.rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": self.local,
+              "pci_bus": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+              "uuid": str(getattr(p, "uuid", "")), "name": p.name}
+        if self.world == 1:
+            return {"ranks": [me], "distinct_devices": 1, "comm_world": 1, "rccl_world": None, "backend": None}
+        ranks = [None] * self.world
+        dist.all_gather_object(ranks, me)
+        backend = str(dist.get_backend())
+        comm = dist.get_world_size()
+        rccl = None
+        if backend == "nccl":
+            t = torch.ones(1, device=self.dev)
+            dist.all_reduce(t)
+            rccl = int(t.item())
+        distinct = len({(r["pci_bus"], r["uuid"]) for r in ranks})
+        out = {"ranks": ranks, "distinct_devices": distinct, "comm_world": comm, "rccl_world": rccl,
+               "backend": backend}
+        if comm != self.world or [r["rank"] for r in ranks] != list(range(self.world)):
+            raise SystemExit(f"bench.py: communicator of {comm} ranks for WORLD_SIZE={self.world}: {ranks}")
+        if backend == "nccl" and (distinct != self.world or rccl != self.world):
+            raise SystemExit(f"bench.py: {self.world} ranks but {distinct} distinct devices / RCCL all-reduce "
+                             f"over {rccl}: {ranks}")
+        if backend != "nccl":
+            out["rehearsal"] = f"{backend} collectives, {distinct} device(s) for {self.world} ranks"
+        return out
 
     def max_over_ranks(self, x: float) -> float:
         if self.world == 1:
@@ -468,6 +505,7 @@ def main():
         sys.exit(rc)
     c = Ctx(a)
     world, rank = c.world, c.rank
+    devices = c.rank_devices()  # before any measurement: a wrong layout never prints a value
     if a.mode == "exact":
         import vsg
         from vsg import datagen as G
@@ -475,7 +513,7 @@ def main():
         lo, hi = rank * a.rows // world, (rank + 1) * a.rows // world
         x = vsg.datagen_device("clustered", hi - lo, a.dim, bs, ms, start=lo)
         q = vsg.datagen_device("clustered", a.batch, a.dim, qs, ms)
-        run_exact(a, x, q, lo, hi, world, rank, c.local, c.dev, c.stream, c.barrier, c.max_over_ranks)
+        run_exact(a, x, q, lo, hi, world, rank, c.local, c.dev, c.stream, c.barrier, c.max_over_ranks, devices)
         if world > 1:
             c.dist.destroy_process_group()
         return
@@ -509,6 +547,7 @@ def main():
         "value": round(head["qps"], 1),
         "unit": "queries/s",
         "n_gpus": world,
+        "devices": devices,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(head["ms_per_step"], 3),
@@ -579,6 +618,9 @@ def main():
     # memory, as usearch's add(key, &[f32]) and search(&[f32], k) do, usearch.rs:221, 276)
     if world == 1 and a.host_abi_leg and a.mode == "hnsw":
         out["host_abi"] = host_abi_leg(c, head)
+    # the drop-in's serving path through the actor (single-query messages, N=1)
+    if world == 1 and a.actor_leg and a.mode == "hnsw":
+        out["actor_serving"] = actor_serving_leg(a, head["ef"])
     # CPU baseline (rank 0, N=1 only): oracle/ restatement of usearch
     if world == 1 and rank == 0 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(a, head["index"], head["q"], head["ef"], head["x"], head["gt"])
@@ -595,7 +637,7 @@ def main():
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 
 
-def run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_over_ranks):
+def run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_over_ranks, devices=None):
     """Brute-force mode: one step = exact top-k of a batch of
     queries over the whole index on the f32 matrix cores; roofline bound = MFMA."""
     import torch
@@ -644,7 +686,7 @@ def run_exact(a, x, q, lo, hi, world, rank, local, dev, stream, barrier, max_ove
     out = {
         "metric": f"brute-force kNN QPS (exact, {'f32 MFMA' if mfma else 'VALU'}), {a.rows} x {a.dim} {a.quant} "
                   f"{a.metric}, batch {a.batch}",
-        "value": round(qps, 1), "unit": "queries/s", "n_gpus": world, "steps": a.steps,
+        "value": round(qps, 1), "unit": "queries/s", "n_gpus": world, "devices": devices, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(1000 * elapsed / a.steps, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic clustered-latent embeddings generated in HBM (vsg/datagen.py)",
@@ -756,11 +798,49 @@ def abi_leg(c):
            "build_device_s_max_shard": round((st["build_insert_ns"] + st["build_sort_ns"] +
                                               st["build_reverse_ns"]) * 1e-9, 4),
            "shards": world, "devices": devices, "answer_device": c.local,
+           # hipDeviceCanAccessPeer of every (shard device -> answering device) gather
+           # this leg used (the copies take the peer path where it is 1, else staged)
+           "peer_access": [[d, c.local, bool(torch.cuda.can_device_access_peer(d, c.local))]
+                           for d in sorted(set(devices)) if d != c.local],
            "shard_rows": [idx.shard(g).size() for g in range(world)],
            "note": "one process, vsg_sharded_* C ABI over all N devices: host-buffer add (PCIe included in "
                    "build_seconds), device-resident queries, peer-DMA gather + HIP merge"}
     idx.close()
     return res
+
+
+def actor_serving_leg(a, ef, clients_list=(512, 2048), total=51200):
+    """The drop-in's own serving path: the reference answers one Ann
+    per message through a oneshot (/root/reference/src/index/usearch.rs:251-306), so
+    closed-loop clients each keep one single-query vsg_actor_ann_cb in flight on an actor
+    over the headline index (same rows, parameters and level seed, built in the child)
+    at the headline ef; the actor coalesces them into batched GPU searches.  Runs
+    tools/actor_load as a child process (no exec): QPS, latency p50 / p99 and whether
+    every answer equals the batched search's."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "actor_load")
+    if not os.path.exists(exe):
+        return {"error": "tools/actor_load not built (__graft_entry__.build)"}
+    out = {"note": "closed-loop clients of single-query vsg_actor_ann_cb (completion = the reference's "
+                   "oneshot), one actor worker; index rebuilt in the child with the headline rows/seed",
+           "ef": ef}
+    for cl in clients_list:
+        cmd = [exe, str(a.rows), str(a.dim), str({"l2sq": 0, "ip": 1, "cos": 2}[a.metric]), str(cl),
+               str(max(1, total // cl)), str(a.k), str(ef), "0", "0", "1", str(0x5EED)]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            if r.returncode != 0 or not line:
+                out[f"clients_{cl}"] = {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+                continue
+            j = json.loads(line[-1])
+            out[f"clients_{cl}"] = {"qps": j["actor_qps"], "lat_us_p50": j["lat_us_p50"],
+                                    "lat_us_p99": j["lat_us_p99"], "mean_batch": j["mean_batch"],
+                                    "mismatch_vs_batched": j["mismatch_vs_batched"], "errors": j["errors"],
+                                    "batched_qps_same_queries": j["batched_qps"]}
+        except subprocess.TimeoutExpired:
+            out[f"clients_{cl}"] = {"error": "timeout"}
+    return out
 
 
 def host_abi_leg(c, head):

@@ -141,8 +141,11 @@ int vsg_index_contains(const vsg_index_t* index, uint64_t key);
  * oldest removal first (the entry point's slot is skipped while it is the entry
  * point); such a slot keeps its level and the other nodes' links into it, gets
  * the new key and vector and is re-linked in place, before the rest of the call
- * is appended.  The reference's replace is remove + add (usearch.rs:214-221), so
- * an upsert stream recycles slots instead of growing.  Rules in
+ * is appended.  The call acts as that many single adds: the reused slots are
+ * re-linked in call order, in consecutive batches each staged right before it
+ * (later reused slots keep their old vectors and links meanwhile).  The
+ * reference's replace is remove + add (usearch.rs:214-221), so an upsert stream
+ * recycles slots instead of growing (vsg_index_replace).  Rules in
  * oracle/vsg_oracle.h orc_hnsw_add; VSG_FLAG_NO_SLOT_REUSE turns it off. */
 int vsg_index_add(vsg_index_t* index, const uint64_t* keys, const float* vectors, size_t n);
 /* Same, with `vectors` already in device memory (f32, n x dimensions). */
@@ -154,6 +157,35 @@ int vsg_index_add_device(vsg_index_t* index, const uint64_t* keys, const float* 
  * the back of the free ring for reuse by later adds; *n_removed (optional)
  * counts keys that were live. */
 int vsg_index_remove(vsg_index_t* index, const uint64_t* keys, size_t n, size_t* n_removed);
+/* replaces the AddOrReplace body of src/index/usearch.rs:214-221 (`if remove {
+ * idx.remove(key) }` then `idx.add(key, &embedding)`, one message before the next,
+ * fed per key by src/monitor_items.rs:56-80), batched: for each i in order, key
+ * i is removed if live and then added with vector i.  Results follow the
+ * one-message-at-a-time sequence -- every key takes the slot that sequence gives
+ * it (free ring, oldest first), keys may repeat (a later message wins) -- while the
+ * GPU applies the messages in chunks of consecutive keys: a chunk removes its live
+ * keys and re-links their freed slots as one batch, so the rest of the stream
+ * stays live with its old vectors meanwhile.  Chunk sizes: batch != 0 => at most
+ * `batch`; 0 => max(1, size / 4096) for keys re-linked into free slots (every key
+ * alone below 8,192 live rows: exactly the sequence) and max(1, size / 8) for keys
+ * appended as new rows (the bulk build's batching).  Chunk boundaries depend on
+ * the keys and the index state only, never on timing.  flags
+ * VSG_REPLACE_HOLD_TAIL: an incomplete last chunk (fewer keys than its size, and
+ * not ended by a following key) is left unapplied: its keys get status
+ * VSG_HELD and *n_applied (optional) counts the keys applied -- a caller
+ * streaming messages in pieces re-submits the held ones, in order, ahead of the
+ * next piece and gets the chunks an uncut stream gets (the actor does).  status
+ * (optional, n entries): per key VSG_OK, VSG_HELD or the
+ * error of its chunk; a failed chunk does not stop the others (the reference
+ * fails per vector, usearch.rs:221-232); returns the first error.  A key whose
+ * add failed is absent afterwards (the reference drops its mapping, :230-232). */
+#define VSG_REPLACE_HOLD_TAIL 1u
+#define VSG_HELD 6 /* status of a key left unapplied under VSG_REPLACE_HOLD_TAIL (not an error) */
+int vsg_index_replace(vsg_index_t* index, const uint64_t* keys, const float* vectors, size_t n, size_t batch,
+                      uint32_t flags, int* status, size_t* n_applied);
+/* Same, with `vectors` in device memory (f32, n x dimensions) ordered after `stream`. */
+int vsg_index_replace_device(vsg_index_t* index, const uint64_t* keys, const float* vectors_device, size_t n,
+                             size_t batch, int* status, void* stream);
 /* The free ring (usearch index_dense free_keys_): removed slots, oldest removal
  * first -- exactly the index's removed slots.  Copies up to `cap` slot ids to
  * `out` (may be NULL) and returns how many there are. */
@@ -179,7 +211,9 @@ int vsg_index_set_f16_traversal(vsg_index_t* index, int enable);
  * step on level 1 by a beam of width min(upper_ef, ef) whose whole result set
  * seeds the level-0 beam (register search kernel).  0 or 1 = usearch's greedy
  * descent (default).  Raises recall at a given ef; results are no longer the
- * usearch traversal's, so parity is by recall, not bit-exact. */
+ * usearch traversal's, so parity is by recall, not bit-exact.  An index holding
+ * removed entries searches with the greedy descent (its overflow re-run walks a
+ * sorted list in device memory that has no multi-entry form). */
 int vsg_index_set_upper_ef(vsg_index_t* index, size_t upper_ef);
 
 /* Device-resident variants: queries (f32 nq x dimensions), outputs and counts
@@ -311,6 +345,12 @@ uint32_t vsg_sharded_route(const vsg_sharded_t* index, uint64_t key);
 vsg_index_t* vsg_sharded_shard(vsg_sharded_t* index, size_t g);
 int vsg_sharded_add(vsg_sharded_t* index, const uint64_t* keys, const float* vectors, size_t n);
 int vsg_sharded_remove(vsg_sharded_t* index, const uint64_t* keys, size_t n, size_t* n_removed);
+/* vsg_index_replace on every shard concurrently (each key's messages meet on its
+ * shard, which applies its own sub-stream in order).  With VSG_REPLACE_HOLD_TAIL
+ * each shard holds its own tail (status VSG_HELD; re-submitted in order, they
+ * lead that shard's next sub-stream). */
+int vsg_sharded_replace(vsg_sharded_t* index, const uint64_t* keys, const float* vectors, size_t n, size_t batch,
+                        uint32_t flags, int* status, size_t* n_applied);
 /* as vsg_index_search / _exact_search: every shard returns its top k */
 int vsg_sharded_search(vsg_sharded_t* index, const float* queries, size_t nq, size_t k, size_t ef,
                        uint64_t* out_keys, float* out_distances, size_t* out_counts);

@@ -57,6 +57,7 @@ def lib():
         L.orc_hnsw_add.argtypes = [P, P, P, sz, C.c_int]
         L.orc_hnsw_remove.restype = sz
         L.orc_hnsw_remove.argtypes = [P, P, sz]
+        L.orc_hnsw_replace.argtypes = [P, P, P, sz, P]
         L.orc_hnsw_free_list.restype = sz
         L.orc_hnsw_free_list.argtypes = [P, P, sz]
         L.orc_hnsw_set_slot_reuse.argtypes = [P, C.c_int]
@@ -155,6 +156,15 @@ class HnswOracle:
     def remove(self, keys):
         keys = np.ascontiguousarray(keys, np.uint64)
         return lib().orc_hnsw_remove(self.h, _p(keys), len(keys))
+
+    def replace(self, keys, vecs):
+        """The reference's AddOrReplace stream one message at a time (usearch.rs:
+        214-221): per key, remove if live, then add.  Returns per-key status."""
+        keys = np.ascontiguousarray(keys, np.uint64)
+        vecs = np.ascontiguousarray(vecs, np.float32).reshape(len(keys), self.dim)
+        st = np.zeros(len(keys), np.int32)
+        lib().orc_hnsw_replace(self.h, _p(keys), _p(vecs), len(keys), _p(st))
+        return st
 
     def free_list(self):
         """The free ring (usearch index_dense free_keys_), oldest removal first."""

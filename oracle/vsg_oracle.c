@@ -782,7 +782,15 @@ static void clear_rows(orc_hnsw* h, uint32_t s) {
     }
 }
 
+/* s1: a caller-owned scratch for a single-threaded call (orc_hnsw_replace reuses
+ * one across its keys instead of allocating a slot-sized stamp array per key) */
+static int add_impl(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n, int threads, scratch_t* s1);
+
 int orc_hnsw_add(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n, int threads) {
+    return add_impl(h, keys, vecs, n, threads, NULL);
+}
+
+static int add_impl(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n, int threads, scratch_t* s1) {
     if (n == 0) return 0;
     /* validate: no reserved key, no live duplicate, no duplicate inside batch */
     for (size_t i = 0; i < n; ++i) {
@@ -825,16 +833,9 @@ int orc_hnsw_add(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n,
             return 2;
         }
     }
-    /* stage the reused slots (index_gt::update): new key and vector, every row
-     * cleared, level kept, live again */
-    for (size_t i = 0; i < r; ++i) {
-        const uint32_t sl = list[i];
-        memcpy(h->vecs + (size_t)sl * h->dim, vecs + i * h->dim, h->dim * sizeof(float));
-        h->keys[sl] = keys[i];
-        h->removed[sl] = 0;
-        km_put(&h->km, keys[i], sl);
-        clear_rows(h, sl);
-    }
+    /* the reused slots' keys are mapped now (the call is accepted); each slot is
+     * staged right before its own re-link below */
+    for (size_t i = 0; i < r; ++i) km_put(&h->km, keys[i], list[i]);
     size_t base = h->slots;
     size_t need_upper = 0;
     for (size_t i = 0; i < na; ++i) {
@@ -867,25 +868,51 @@ int orc_hnsw_add(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n,
     h->live += n;
 
     /* insertion order: the reused slots (call order), then the appended ones */
-    threads = resolve_threads(threads);
-    if ((size_t)threads > n) threads = (int)n;
+    threads = s1 ? 1 : resolve_threads(threads);
+    if ((size_t)threads > na) threads = (int)na;
     if (threads < 1) threads = 1;
-    scratch_t* scr = (scratch_t*)malloc(sizeof(scratch_t) * threads);
-    for (int t = 0; t < threads; ++t) scratch_init(&scr[t], h->cap, h->efC > h->ef ? h->efC : h->ef, h->M0);
-    if (threads == 1) {
-        for (size_t i = 0; i < n; ++i) insert_slot(h, list[i], &scr[0], 0);
+    scratch_t* scr = s1;
+    if (s1) {
+        if (s1->stamp_cap < h->cap) { /* the index grew: a larger stamp array */
+            free(s1->stamp);
+            s1->stamp = (uint32_t*)calloc(h->cap, sizeof(uint32_t));
+            s1->stamp_cap = h->cap;
+            s1->gen = 0;
+        }
     } else {
+        scr = (scratch_t*)malloc(sizeof(scratch_t) * threads);
+        for (int t = 0; t < threads; ++t) scratch_init(&scr[t], h->cap, h->efC > h->ef ? h->efC : h->ef, h->M0);
+    }
+    /* Reused slots one key at a time, as a sequence of single adds (index_dense
+     * add_ pops ONE free slot per call and runs index_gt::update on it): the slot
+     * gets its new key and vector, its rows (every level) are cleared, it is live
+     * again -- and it is re-linked before the next key's slot is touched, so the
+     * slots later in the call still hold their old vectors and links.  Always
+     * sequential (their order is the call's). */
+    for (size_t i = 0; i < r; ++i) {
+        const uint32_t sl = list[i];
+        memcpy(h->vecs + (size_t)sl * h->dim, vecs + i * h->dim, h->dim * sizeof(float));
+        h->keys[sl] = keys[i];
+        h->removed[sl] = 0;
+        clear_rows(h, sl);
+        insert_slot(h, sl, &scr[0], 0);
+    }
+    if (threads == 1) {
+        for (size_t i = r; i < n; ++i) insert_slot(h, list[i], &scr[0], 0);
+    } else if (na) {
         /* the very first node must exist before concurrent inserts start */
-        size_t start = 0;
+        size_t start = r;
         if (h->entry == ORC_EMPTY) {
-            insert_slot(h, list[0], &scr[0], 0);
-            start = 1;
+            insert_slot(h, list[start], &scr[0], 0);
+            ++start;
         }
         add_ctx c = {h, list + start, scr};
         parallel_for(n - start, threads, add_one, &c);
     }
-    for (int t = 0; t < threads; ++t) scratch_free(&scr[t]);
-    free(scr);
+    if (!s1) {
+        for (int t = 0; t < threads; ++t) scratch_free(&scr[t]);
+        free(scr);
+    }
     free(list);
     return 0;
 }
@@ -902,6 +929,25 @@ size_t orc_hnsw_remove(orc_hnsw* h, const uint64_t* keys, size_t n) {
         }
     }
     return r;
+}
+
+/* The reference's AddOrReplace stream, one message at a time
+ * (src/index/usearch.rs:214-221: `if remove { idx.remove(key) }` then
+ * `idx.add(key, &embedding)`, each message before the next).  status[i]
+ * (optional) = the add's code for message i; a failed add fails only its own
+ * vector (usearch.rs:221-232). */
+int orc_hnsw_replace(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n, int* status) {
+    int first = 0;
+    scratch_t scr;
+    scratch_init(&scr, h->cap, h->efC > h->ef ? h->efC : h->ef, h->M0);
+    for (size_t i = 0; i < n; ++i) {
+        (void)orc_hnsw_remove(h, keys + i, 1);
+        const int rc = add_impl(h, keys + i, vecs + i * h->dim, 1, 1, &scr);
+        if (status) status[i] = rc;
+        if (rc && !first) first = rc;
+    }
+    scratch_free(&scr);
+    return first;
 }
 
 size_t orc_hnsw_free_list(const orc_hnsw* h, uint32_t* out, size_t cap) {

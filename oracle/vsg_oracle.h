@@ -88,10 +88,13 @@ void orc_hnsw_params(const orc_hnsw* h, size_t* M, size_t* M0, size_t* efC,
  * first keys of the call take removed slots from the free ring, oldest
  * removal first (usearch free_keys_ is a FIFO ring_gt), skipping the slot of
  * the current entry point; the rest are appended.  A reused slot keeps its
- * level; at the start of the call it gets its new key and vector, its rows
- * (every level) are cleared and it is live again; other nodes' links into it
- * stay.  Then the reused slots are re-linked in call order, then the appended
- * slots inserted -- each as connect_node_across_levels_ from the entry point.
+ * level; other nodes' links into it stay.  The call is a sequence of single
+ * adds (usearch's add_ pops one slot per call): in call order, each reused slot
+ * gets its new key and vector, its rows (every level) are cleared, it is live
+ * again and it is re-linked -- before the next key's slot is touched, so later
+ * reused slots still hold their old vectors and links meanwhile (round 6; round
+ * 5 staged every reused slot of the call first).  Then the appended slots are
+ * inserted -- each as connect_node_across_levels_ from the entry point.
  * Rules beyond a plain insert (the usearch v2 series restated):
  *   - a node is never a candidate of its own insertion (greedy descent and
  *     beam skip it; usearch asserts "Self-loops are impossible");
@@ -108,6 +111,11 @@ int orc_hnsw_add(orc_hnsw* h, const uint64_t* keys, const float* vecs,
 /* Tombstone keys; returns number removed.  Each removed slot joins the back of
  * the free ring (usearch index_dense_gt::remove: free_keys_.push(slot)). */
 size_t orc_hnsw_remove(orc_hnsw* h, const uint64_t* keys, size_t n);
+/* The reference's upsert stream strictly one message at a time
+ * (src/index/usearch.rs:214-221): per key, remove it if live, then add it
+ * (sequential, single-threaded).  status[i] (optional) = that add's code;
+ * returns the first non-zero code (a failed add fails only its own vector). */
+int orc_hnsw_replace(orc_hnsw* h, const uint64_t* keys, const float* vecs, size_t n, int* status);
 /* The free ring, oldest first: writes min(count, cap) slots, returns count.
  * Invariant: the ring holds exactly the removed slots. */
 size_t orc_hnsw_free_list(const orc_hnsw* h, uint32_t* out, size_t cap);

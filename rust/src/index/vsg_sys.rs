@@ -15,6 +15,8 @@ pub const VSG_ENOMEM: c_int = 2;
 pub const VSG_EDUPKEY: c_int = 3;
 pub const VSG_EDEVICE: c_int = 4;
 pub const VSG_EUNSUPPORTED: c_int = 5;
+pub const VSG_HELD: c_int = 6;
+pub const VSG_REPLACE_HOLD_TAIL: u32 = 1;
 
 pub const VSG_METRIC_L2SQ: u32 = 0;
 pub const VSG_METRIC_IP: u32 = 1;
@@ -171,6 +173,11 @@ extern "C" {
                                 n: usize, stream: *mut c_void) -> c_int;
     // usearch::Index::remove (usearch.rs:215, 245)
     pub fn vsg_index_remove(index: *mut vsg_index_t, keys: *const u64, n: usize, n_removed: *mut usize) -> c_int;
+    // the AddOrReplace stream (usearch.rs:214-221): per key remove-if-live then add, in order
+    pub fn vsg_index_replace(index: *mut vsg_index_t, keys: *const u64, vectors: *const f32, n: usize, batch: usize,
+                             flags: u32, status: *mut c_int, n_applied: *mut usize) -> c_int;
+    pub fn vsg_index_replace_device(index: *mut vsg_index_t, keys: *const u64, vectors_device: *const f32, n: usize,
+                                    batch: usize, status: *mut c_int, stream: *mut c_void) -> c_int;
     pub fn vsg_index_free_slots(index: *const vsg_index_t, out: *mut u32, cap: usize) -> usize;
     // usearch::Index::search (usearch.rs:276), batched; rows padded with VSG_NO_KEY / +inf
     pub fn vsg_index_search(index: *mut vsg_index_t, queries: *const f32, nq: usize, k: usize, ef: usize,
@@ -217,6 +224,8 @@ extern "C" {
     pub fn vsg_sharded_shard(index: *mut vsg_sharded_t, g: usize) -> *mut vsg_index_t;
     pub fn vsg_sharded_add(index: *mut vsg_sharded_t, keys: *const u64, vectors: *const f32, n: usize) -> c_int;
     pub fn vsg_sharded_remove(index: *mut vsg_sharded_t, keys: *const u64, n: usize, n_removed: *mut usize) -> c_int;
+    pub fn vsg_sharded_replace(index: *mut vsg_sharded_t, keys: *const u64, vectors: *const f32, n: usize,
+                               batch: usize, flags: u32, status: *mut c_int, n_applied: *mut usize) -> c_int;
     pub fn vsg_sharded_search(index: *mut vsg_sharded_t, queries: *const f32, nq: usize, k: usize, ef: usize,
                               out_keys: *mut u64, out_distances: *mut f32, out_counts: *mut usize) -> c_int;
     pub fn vsg_sharded_exact_search(index: *mut vsg_sharded_t, queries: *const f32, nq: usize, k: usize,

@@ -578,35 +578,77 @@ static void test_read_workers_overlap() {
     }
 }
 
-// 6) replace segments: a run of replaces is applied in segments of at most
-//    live / replace_div removes (each followed by its adds), so a re-linked key
-//    sees all but a small fraction of the index live, as the reference's
-//    one-message-at-a-time replace does; the final state is the sequential one
-static void test_replace_segments() {
+// 8) replace runs: every run of AddOrReplace messages reaches the backend as one
+//    replace call in submission order (keys may repeat; vsg_index_replace applies
+//    them as the reference's one-message-at-a-time remove + add), every run of
+//    removes as one remove call; the final state is the sequential one
+struct ReplMock final : vsg::ActorBackend {
+    std::map<uint64_t, float> rows;
     std::vector<Call> log;
-    std::vector<size_t> res;
-    auto* m = new Mock(2, 8, &log, &res, 0);
-    Mock* mp = m;
+    size_t cap = 0;
+    size_t dimensions() const override { return 1; }
+    size_t size() const override { return rows.size(); }
+    size_t capacity() const override { return cap; }
+    size_t expansion_search() const override { return 4; }
+    bool contains(uint64_t k) const override { return rows.count(k) != 0; }
+    int reserve(size_t c) override {
+        cap = std::max(cap, c);
+        return 0;
+    }
+    int add(const uint64_t*, const float*, size_t n) override {
+        log.push_back({'a', n, 0, 0});
+        return 4;
+    }
+    int remove(const uint64_t* k, size_t n, size_t* r) override {
+        log.push_back({'r', n, 0, 0});
+        size_t c = 0;
+        for (size_t i = 0; i < n; ++i) c += rows.erase(k[i]);
+        if (r) *r = c;
+        return 0;
+    }
+    int replace(const uint64_t* k, const float* v, size_t n, size_t, bool, int* status) override {
+        log.push_back({'p', n, 0, 0});
+        for (size_t i = 0; i < n; ++i) {
+            rows[k[i]] = v[i];
+            status[i] = 0;
+        }
+        return 0;
+    }
+    int search(const float*, size_t, size_t, size_t, uint64_t*, float*, size_t*) override { return 0; }
+};
+
+static void test_replace_runs() {
+    auto* m = new ReplMock;
+    ReplMock* mp = m;
     vsg::ActorConfig cfg;
     cfg.reserve_increment = 4096;
     vsg::Actor a(std::unique_ptr<vsg::ActorBackend>(m), cfg);
     CHECK(a.init() == 0);
-    float v[2] = {1.f, 2.f};
-    for (uint64_t k = 0; k < 640; ++k) a.add_or_replace(k, v);
+    for (uint64_t k = 0; k < 640; ++k) {
+        const float v = 1.f;
+        a.add_or_replace(k, &v);
+    }
     CHECK(a.flush() == 0);
-    log.clear();
-    float w[2] = {3.f, 4.f};
-    for (uint64_t k = 0; k < 100; ++k) a.add_or_replace(k, w);
+    mp->log.clear();
+    for (uint64_t k = 0; k < 100; ++k) {
+        const float w = 3.f;
+        a.add_or_replace(k, &w);
+    }
+    const float x = 5.f, y = 7.f, z = 9.f;
+    a.remove(5);
+    a.add_or_replace(5, &x);
+    a.add_or_replace(7, &y);
+    a.add_or_replace(7, &z);  // repeated inside one run: the later message wins
     CHECK(a.flush() == 0);
-    size_t removes = 0, removed = 0;
-    for (const Call& c : log)
-        if (c.op == 'r') {
-            ++removes;
-            removed += c.n;
-            CHECK(c.n <= 640 / 64);
-        }
-    CHECK(removed == 100 && removes >= 10);
-    CHECK(mp->rows.size() == 640 && mp->rows[5][0] == 3.f && mp->rows[300][0] == 1.f);
+    size_t replaced = 0, removed = 0;
+    for (const Call& c : mp->log) {
+        CHECK(c.op != 'a');  // adds only through replace
+        if (c.op == 'p') replaced += c.n;
+        if (c.op == 'r') removed += c.n;
+    }
+    CHECK(replaced == 103 && removed == 1);
+    CHECK(mp->rows.size() == 640 && mp->rows[5] == 5.f && mp->rows[7] == 9.f && mp->rows[50] == 3.f &&
+          mp->rows[300] == 1.f);
 }
 
 int main() {
@@ -619,7 +661,7 @@ int main() {
     test_add_errors_swallowed();
     test_add_completions();
     test_auto_compaction();
-    test_replace_segments();
+    test_replace_runs();
     std::printf("ok\n");
     return 0;
 }

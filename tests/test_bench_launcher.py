@@ -42,6 +42,12 @@ def test_gpus_2_launches_two_ranks():
     abi = r["sharded_abi"]
     assert abi["shards"] == 2 and abi["devices"] == [0, 0] and sum(abi["shard_rows"]) == 100000
     assert abi["recall_at_10"] >= 0.95 and abi["qps"] > 0 and abi["build_vectors_per_s"] > 0
+    assert abi["peer_access"] == []  # every shard on the answering device here
+    # which device every rank ran on: gathered over the communicator
+    dv = r["devices"]
+    assert dv["comm_world"] == 2 and dv["backend"] == "gloo" and [x["rank"] for x in dv["ranks"]] == [0, 1]
+    assert dv["distinct_devices"] == 1 and "rehearsal" in dv and dv["rccl_world"] is None
+    assert all(x["pci_bus"] == dv["ranks"][0]["pci_bus"] for x in dv["ranks"])
 
 
 @pytest.mark.gpu
@@ -66,6 +72,7 @@ def test_gpus_4_hybrid_layout():
     assert r["shard_mode"]["shards_per_group"] == 4 and r["shard_mode"]["queries_per_step"] == 1000
     assert r["replica_mode"]["groups"] == 4 and r["replica_mode"]["queries_per_step"] == 4000
     assert r["sharded_abi"]["shards"] == 4
+    assert r["devices"]["comm_world"] == 4 and len(r["devices"]["ranks"]) == 4
 
 
 @pytest.mark.gpu
@@ -83,6 +90,7 @@ def test_gpus_1_line_fields():
     assert len(lines) == 1, out.stdout
     r = lines[0]
     assert r["n_gpus"] == 1 and r["value"] > 0 and r["config"]["recall_at_10"] >= 0.95
+    assert r["devices"]["distinct_devices"] == 1 and r["devices"]["ranks"][0]["device"] == 0
     assert 0 < r["roofline"]["frac"] <= 1.0 and r["roofline"]["kernel"] == "hnsw_search_reg_kernel"
     cs = r["concurrent_streams"]
     assert cs["streams"] == 2 and cs["qps"] > 0 and cs["results_equal_single_stream"] is True

@@ -187,54 +187,74 @@ def test_c2_gpu_search_on_oracle_graph(c2, ef):
 
 
 # ---------------------------------------------------------------- churn (last) --
-# The reference's replace is remove + add of the same key (usearch.rs:183-196, 214-221);
-# usearch re-links the freed slot on the next add (index_dense free-slot reuse).  These
-# tests run after every test above (they mutate the module's two indexes): 10 % of the
-# rows replaced by new points of the same distribution, on both sides, then the ±0.5 %
-# bar again at the same two ef values against a fresh exact ground truth.
+# The reference's replace is remove + add of the same key, one message at a time
+# (usearch.rs:183-196, 214-221, fed per key by monitor_items.rs:56-80); usearch re-links
+# the freed slot on the next add (index_dense free-slot reuse).  These tests run after
+# every test above (they mutate the module's two indexes): 10 % of the rows replaced
+# by new points of the same distribution -- on the GPU through vsg_index_replace (the
+# default chunks: live / 4096 = 244 keys removed and re-linked as one batch at a time),
+# on the oracle strictly one message at a time (remove([k]); add([k]), the reference's
+# sequence) -- then the +-0.5 % bar again at the same two ef values against a fresh
+# exact ground truth.
 NREP = N // 10
 
 
 @pytest.fixture(scope="module")
 def churned(c2):
+    import time
+
     import torch
     gpu, orc = c2["gpu"], c2["orc"]
     bs, qs, ms = G.config_seeds(1)
     rng = np.random.default_rng(0xC4A7)
-    keys = np.sort(rng.choice(N, NREP, replace=False)).astype(np.uint64)
+    keys = rng.choice(N, NREP, replace=False).astype(np.uint64)  # a stream in random key order
     newx = vsg.datagen_device("clustered", NREP, DIM, bs, ms, start=N)  # rows N.. of the same stream
-    assert gpu.remove(keys) == NREP and orc.remove(keys) == NREP
-    ring_g, ring_o = gpu.free_slots(), orc.free_list()
-    np.testing.assert_array_equal(ring_g, ring_o)  # same removal order on both sides
     slots_before = gpu.graph_info()["slots"]
-    gpu.add_device(keys, newx)
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = gpu.replace_device(keys, newx)
+    torch.cuda.synchronize()
+    t_gpu = time.perf_counter() - t0
+    assert (st == 0).all()
     nh = newx.cpu().numpy()
     O.set_fast_metric(True)
     try:
-        orc.add(keys, nh, threads=_cores())
+        t0 = time.perf_counter()
+        sto = orc.replace(keys, nh)
+        t_orc = time.perf_counter() - t0
     finally:
         O.set_fast_metric(False)
+    assert (sto == 0).all()
+    print(f"C2 churn: {NREP} replaces, GPU replace call {t_gpu:.2f} s, oracle one at a time {t_orc:.1f} s")
     gt_k = gpu.search_device(c2["q"], K, exact=True)[0]
     torch.cuda.synchronize()
-    return {"gt": gt_k.cpu().numpy().view(np.uint64), "slots_before": slots_before, "ring": ring_g}
+    return {"gt": gt_k.cpu().numpy().view(np.uint64), "slots_before": slots_before, "keys": keys}
 
 
 def test_c2_churn_reuses_slots(c2, churned):
-    """Every replaced key took a freed slot: no growth, an empty ring (the entry
-    point's slot aside), the same slots on both sides."""
+    """Every replaced key took a freed slot (its own, as in the sequence; the entry
+    point's key, if replaced, is appended while its slot waits in the ring): no other
+    growth, the same ring and the same slot for every key on both sides."""
     gpu, orc = c2["gpu"], c2["orc"]
-    assert gpu.graph_info()["slots"] == churned["slots_before"] == N
+    assert churned["slots_before"] == N
+    assert gpu.graph_info()["slots"] <= N + 1
     assert gpu.size() == N and orc.size() == N
     left_g, left_o = gpu.free_slots(), orc.free_list()
-    assert len(left_g) <= 1 and len(left_o) <= 1
+    np.testing.assert_array_equal(left_g, left_o)
+    assert len(left_g) <= 1
     assert gpu.stats()["slots_reused"] >= NREP - 1
+    kg = gpu.export()["keys"]
+    ko = orc.export()["keys"]
+    live = np.ones(len(kg), bool)
+    live[left_g.astype(np.int64)] = False
+    np.testing.assert_array_equal(kg[live], ko[live])  # same key in every slot
 
 
 @pytest.mark.parametrize("ef", [36, 128])
 def test_c2_churn_recall_vs_oracle(c2, churned, ef):
-    """After replacing 10 % of the rows (remove + add of the same keys, freed slots
-    re-linked in place), GPU recall@10 within +-0.5 % of the oracle's at matched ef."""
+    """After replacing 10 % of the rows (GPU: the batched replace call; oracle: the
+    reference's one-replace-at-a-time sequence), GPU recall@10 within +-0.5 % of the
+    oracle's at matched ef."""
     gpu, orc, qh, gt = c2["gpu"], c2["orc"], c2["qh"], churned["gt"]
     O.set_fast_metric(True)
     try:
@@ -242,5 +262,5 @@ def test_c2_churn_recall_vs_oracle(c2, churned, ef):
     finally:
         O.set_fast_metric(False)
     rg = recall(gpu.search(qh, K, ef).keys, gt)
-    print(f"C2 churn 10% ef={ef}: recall GPU {rg:.4f}  oracle {rc:.4f}")
+    print(f"C2 churn 10% ef={ef}: recall GPU replace {rg:.4f}  oracle one at a time {rc:.4f}")
     assert abs(rg - rc) <= 0.005, (ef, rg, rc)

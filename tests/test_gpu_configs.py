@@ -199,8 +199,8 @@ def test_c4_100m128_f16_eight_row_shards_merged():
 def test_c5_1m1536_ip_hnsw_leg():
     """C5's HNSW half (configs[4] "brute-force MFMA path vs HNSW"): 1M x 1536 f32 IP
     HNSW (M=16, efC=128) built on the GPU reaches recall@10 >= 0.95 against the f32
-    MFMA exact ground truth (the probe's operating point, ef 30: 0.952,
-    profiles/r04_configs_c5.jsonl); and at 200k rows the GPU build's recall is within
+    MFMA exact ground truth at the operating point, ef 32 (0.957 in round 5; the probe's
+    ef 30: 0.952, profiles/r04_configs_c5.jsonl); and at 200k rows the GPU build's recall is within
     +-0.5 % of the oracle's own build at matched ef (the north-star bar, two-sided)."""
     import torch
     dim, k, nq = 1536, 10, 5000
@@ -216,7 +216,7 @@ def test_c5_1m1536_ip_hnsw_leg():
     gt = gt.cpu().numpy().view(np.uint64)
     r = {ef: recall(idx.search_device(q, k, ef)[0].cpu().numpy().view(np.uint64), gt, k) for ef in (24, 32, 48, 64)}
     print("C5 1M x 1536 IP HNSW recall@10 by ef:", r)
-    assert r[48] >= 0.95 and r[64] >= r[32] >= r[24] - 0.002
+    assert r[32] >= 0.95 and r[64] >= r[48] >= r[32] >= r[24] - 0.002
     # 200k rows: GPU build vs the oracle build (threaded, host-ISA metrics), same ground truth
     m = 200_000
     xh = x[:m].cpu().numpy()

@@ -110,10 +110,12 @@ def test_reuse_one_node_batches_equal_oracle(metric, M, efc, start, monkeypatch)
 def test_reuse_batched_build_keeps_quality_and_bookkeeping():
     """Batched (default) GPU adds over freed slots, from the oracle's own graph: slots do
     not grow, each reused slot keeps its level, rows hold no self link or duplicate, and
-    recall at matched ef stays within 1 % of the oracle run through the same remove/add
-    calls.  (Both start from one graph: a GPU-built start graph responds to usearch's
-    update semantics a little differently -- ~0.6 % lower after 20 % churn at ef 16 --
-    which is the build's, not the update's; profiles/r05_reuse_variants.jsonl.)"""
+    recall at matched ef stays within 0.5 % of the oracle run through the same remove/add
+    calls -- whose multi-key adds are a sequence of single adds (usearch's add_ pops one
+    free slot per call), while the GPU re-links consecutive batches of graph / 4096
+    keys, each staged right before it.  (Both start from one graph: a GPU-built start
+    graph responds to usearch's update semantics a little differently, which is the
+    build's, not the update's; profiles/r05_reuse_variants.jsonl.)"""
     n, dim = 30000, 64
     x = G.clustered(n + 6000, dim, 311, 9)
     q = G.clustered(500, dim, 312, 9)
@@ -146,7 +148,7 @@ def test_reuse_batched_build_keeps_quality_and_bookkeeping():
     for ef in (16, 64):
         rg, rc = rec(gpu.search(q, 10, ef).keys), rec(h.search(q, 10, ef)[0])
         print(f"churned 30k cos ef={ef}: GPU {rg:.4f} oracle {rc:.4f}")
-        assert abs(rg - rc) <= 0.01, (ef, rg, rc)
+        assert abs(rg - rc) <= 0.005, (ef, rg, rc)
 
 
 def test_reuse_rejected_add_changes_nothing():

@@ -330,6 +330,61 @@ def test_oracle_slot_reuse_matches_literal_usearch_update(metric):
             np.testing.assert_array_equal(d[i][: int(c[i])], np.array(ld, np.float32))
 
 
+@pytest.mark.parametrize("metric", ["l2sq", "ip"])
+def test_oracle_replace_stream_matches_literal_usearch(metric):
+    """The reference's upsert stream one message at a time (/root/reference/src/index/
+    usearch.rs:214-221: remove the live key, then add; fed per key by
+    src/monitor_items.rs:56-80): orc_hnsw_replace against the literal transcription's
+    remove + add_one per message -- existing keys, new keys and a key repeated inside
+    one call, with net deletes interleaved so the free ring is not empty.  Same slot
+    per key, same ring, identical graph and search results."""
+    import usearch_literal as UL
+    n, dim, M, efc = 250, 12, 6, 24
+    x = G.clustered(n + 600, dim, 51, 8)
+    if metric == "ip":
+        x = x / np.linalg.norm(x, axis=1, keepdims=True)
+    q = G.clustered(30, dim, 53, 8)
+    h = O.HnswOracle(dim, metric, M, efc, 16, seed=29)
+    lit = UL.LiteralHnsw(dim, metric, M, efc, seed=29)
+    h.add(np.arange(n), x[:n], threads=1)
+    for i in range(n):
+        lit.add(i, x[i])
+    slot_of = {i: i for i in range(n)}
+    rng = np.random.default_rng(11)
+    row = n
+    for step in range(8):
+        if step % 3 == 2:  # a few net deletes: later adds take these slots first
+            gone = rng.choice(sorted(slot_of), 5, replace=False)
+            h.remove(np.array(gone, np.uint64))
+            lit.remove([slot_of.pop(int(k)) for k in gone])
+        nrep = int(rng.integers(5, 40))
+        keys = rng.integers(0, n + 60, nrep).astype(np.uint64)  # some new, maybe repeated
+        keys[-1] = keys[0]
+        vecs = x[row:row + nrep]
+        row += nrep
+        st = h.replace(keys, vecs)
+        assert (st == 0).all()
+        for key, v in zip(keys.tolist(), vecs):
+            lit.replace(slot_of, key, v)
+        np.testing.assert_array_equal(h.free_list(), np.array(list(lit.free), np.uint32))
+    g = h.export()
+    assert (g["entry"], g["max_level"]) == (lit.entry, lit.max_level)
+    assert h.size() == len(slot_of)
+    key_of = {s: k for k, s in slot_of.items()}
+    for s in range(len(lit.vecs)):
+        assert bool(g["removed"][s]) == (s in lit.removed)
+        if s in key_of:
+            assert int(g["keys"][s]) == key_of[s]
+        for l in range(int(g["levels"][s]) + 1):
+            assert _graph_rows(g, s, l) == lit.links[s][l], (s, l)
+    for ef in (6, 16, 50):
+        k, d, c = h.search(q, 6, ef)
+        for i in range(len(q)):
+            ls, ld = lit.search(q[i], 6, ef)
+            assert k[i][: int(c[i])].tolist() == [key_of[s] for s in ls], (ef, i)
+            np.testing.assert_array_equal(d[i][: int(c[i])], np.array(ld, np.float32))
+
+
 def test_oracle_slot_reuse_rules():
     """The reuse rules on their own: a replaced key takes the OLDEST free slot
     (FIFO), keeps that slot's level, never links to itself, the entry point's

@@ -123,28 +123,41 @@ class LiteralHnsw:
         self.links.append([[] for _ in range(L + 1)])
         return slot
 
-    def add_batch(self, vecs):
-        """One add call of several vectors, as orc_hnsw_add stages it: free slots
-        (oldest removal first, the entry point's skipped) take the first vectors
-        -- new vector, rows cleared, level kept, live again -- the rest are
-        appended; then the reused slots are re-linked in order, then the
-        appended ones.  Returns the slots in call order."""
-        picks, rest = [], deque()
-        while self.free and len(picks) < len(vecs):
-            s = self.free.popleft()
-            (picks if s != self.entry else rest).append(s)
-        self.free = rest + self.free
-        slots = []
-        for s, v in zip(picks, vecs):
-            self.vecs[s] = np.ascontiguousarray(v, np.float32)
+    def add_one(self, vec):
+        """index_dense add_ of one vector: pop the oldest free slot (the entry
+        point's is skipped and keeps its place) and run index_gt::update on it --
+        new vector, rows cleared, level kept, live again, re-linked -- or append
+        when none is free.  Returns the slot."""
+        s = None
+        for i, f in enumerate(self.free):
+            if f != self.entry:
+                s = f
+                del self.free[i]
+                break
+        if s is None:
+            s = self._append(vec)
+        else:
+            self.vecs[s] = np.ascontiguousarray(vec, np.float32)
             self.links[s] = [[] for _ in range(self.levels[s] + 1)]
             self.removed.discard(s)
-            slots.append(s)
-        for v in vecs[len(picks):]:
-            slots.append(self._append(v))
-        for s in slots:
-            self._connect(s)
-        return slots
+        self._connect(s)
+        return s
+
+    def add_batch(self, vecs):
+        """One multi-key add call = that many single adds in call order (each
+        pops one free slot and re-links it before the next key's slot is
+        touched).  Returns the slots in call order."""
+        return [self.add_one(v) for v in vecs]
+
+    def replace(self, slot_of, key, vec):
+        """The reference's AddOrReplace of one message (usearch.rs:214-221):
+        remove the key's live slot if any, then add.  slot_of: key -> slot map
+        (updated); returns the new slot."""
+        if key in slot_of:
+            self.remove([slot_of.pop(key)])
+        s = self.add_one(vec)
+        slot_of[key] = s
+        return s
 
     # connect_node_across_levels_ (index_gt::add / update)
     def _connect(self, slot):

@@ -11,6 +11,8 @@
 //        [mode: 0 = one OS thread per client blocked in vsg_actor_ann; 1 = clients as
 //         completions (vsg_actor_ann_cb, the reference's oneshot reply): each finished
 //         query submits that client's next one from its callback -- no thread per client]
+//        [seed: the index's level seed (bench.py passes its own, so the graph is the
+//         headline index's)]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,6 +50,7 @@ int main(int argc, char** argv) {
     const unsigned wait_us = argc > 8 ? (unsigned)std::atoi(argv[8]) : 0;
     const unsigned readers = argc > 9 ? (unsigned)std::atoi(argv[9]) : 0;
     const int mode = argc > 10 ? std::atoi(argv[10]) : 0;
+    const uint64_t index_seed = argc > 11 ? std::strtoull(argv[11], nullptr, 0) : 1;
     const uint64_t cfg = 2, base_seed = 0x5EED0000 + cfg, q_seed = 0x5EED1000 + cfg, m_seed = 0x5EED2000 + cfg;
 
     vsg_actor_options_t o{};
@@ -56,7 +59,7 @@ int main(int argc, char** argv) {
     o.index.connectivity = 16;
     o.index.expansion_add = 128;
     o.index.expansion_search = (uint32_t)ef;
-    o.index.seed = 1;
+    o.index.seed = index_seed;
     o.max_wait_us = wait_us;
     o.concurrent_reads = readers;
     vsg_actor_t* a = nullptr;

@@ -65,8 +65,10 @@ def parse():
                          "sustained algorithmic bytes / wall)")
     ap.add_argument("--seeds", default="0", help="index seeds (offsets from the default; search mode: the first)")
     ap.add_argument("--phases", action="store_true",
-                    help="build mode, with VSG_LIB_PATH=lib_prof/libvsg.so (make prof): insert-wave "
-                         "clock split into beam / heuristic selection")
+                    help="with VSG_LIB_PATH=lib_prof/libvsg.so (make prof): build mode, insert-wave "
+                         "clock split into beam / heuristic selection; search mode, the register beam's "
+                         "cycles per expansion (select, adjacency wait, visited, row wait, row VALU, "
+                         "admission, compaction)")
     return ap.parse_args()
 
 
@@ -176,6 +178,22 @@ def main():
             nq = max(1, s["search_queries"])
             alg = (s["search_distances"] * row_bytes + s["search_adjacency"] * 2 * a.M * 4) / a.steps
             gbs = alg / (ms_k * 1e-3) / 1e9
+            phases = {}
+            if a.phases:  # VSG_LIB_PATH=lib_prof/libvsg.so: per-expansion cycles of the register beam
+                import ctypes as C
+                from vsg._lib import lib
+                raw = (C.c_uint64 * 32)()
+                lib().vsg_debug_counters_n(idx._h, raw, C.c_size_t(32))
+                nexp = max(1, raw[28] & ((1 << 40) - 1))
+                names = ("select", "adj_wait", "visited", "row_wait", "row_valu", "admit", "compact")
+                phases = {"expansions_per_query": round(nexp / nq, 1),
+                          "compactions_per_query": round((raw[28] >> 40) / nq, 2),
+                          "row_passes_per_expansion": round(raw[29] / nexp, 2),
+                          "cycles_per_expansion": {k: round(raw[20 + i] / nexp, 1) for i, k in enumerate(names)},
+                          "descent_cycles_per_query": round(raw[27] / nq, 1),
+                          "query_cycles": round(raw[30] / nq, 1),
+                          "query_us": round(raw[31] / nq / 100.0, 2),
+                          "clock_ghz": round(raw[30] / max(1, raw[31]) / 10.0, 3)}
             multi = {}
             if a.streams > 1:
                 ss = [torch.cuda.Stream() for _ in range(a.streams)]
@@ -190,7 +208,8 @@ def main():
                 multi = {"streams": a.streams, "streams_ms_per_step": round(wall * 1e3, 3),
                          "streams_qps": round(a.queries / wall, 1),
                          "streams_sustained_frac": round(alg / wall / 1e9 / 8000.0, 4)}
-            print(json.dumps(dict(head, **multi, ef=ef, set=st, kernel_ms=round(ms_k, 3), qps=round(a.queries / ms_k * 1e3, 1),
+            print(json.dumps(dict(head, **multi, **phases, ef=ef, set=st, kernel_ms=round(ms_k, 3),
+                                  qps=round(a.queries / ms_k * 1e3, 1),
                                   dist_per_query=round(s["search_distances"] / nq, 1),
                                   adj_per_query=round(s["search_adjacency"] / nq, 1),
                                   alg_bytes_per_launch=int(alg), achieved_gbs=round(gbs, 1),

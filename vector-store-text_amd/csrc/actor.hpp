@@ -54,6 +54,30 @@ struct ActorBackend {
     virtual int reserve(size_t capacity) = 0;
     virtual int add(const uint64_t* keys, const float* vecs, size_t n) = 0;
     virtual int remove(const uint64_t* keys, size_t n, size_t* removed) = 0;
+    // AddOrReplace messages in order (usearch.rs:214-221: per key, remove the live
+    // copy, then add; vsg_index_replace): status[i] per key, kHeld for a key left
+    // unapplied when hold_tail is set (an incomplete last chunk, re-submitted by the
+    // actor ahead of the next messages).  This default applies them one at a time
+    // and never holds (the mocks of tests/cpp); the GPU backends batch them.
+    static constexpr int kHeld = 6;  // VSG_HELD
+    virtual int replace(const uint64_t* keys, const float* vecs, size_t n, size_t batch, bool hold_tail,
+                        int* status) {
+        (void)batch;
+        (void)hold_tail;
+        int first = 0;
+        const size_t d = dimensions();
+        for (size_t i = 0; i < n; ++i) {
+            int rc = 0;
+            if (contains(keys[i])) rc = remove(keys + i, 1, nullptr);
+            if (rc == 0) rc = add(keys + i, vecs + i * d, 1);
+            status[i] = rc;
+            if (rc && !first) first = rc;
+        }
+        return first;
+    }
+    // the worker restores a captured error message before each failed ann_cb
+    // completion (a completion may run other calls that overwrite the thread's error)
+    virtual void set_error(const std::string& msg) { (void)msg; }
     virtual int search(const float* q, size_t nq, size_t k, size_t ef, uint64_t* keys, float* dist,
                        size_t* counts) = 0;
     virtual const char* last_error() const { return ""; }
@@ -83,17 +107,19 @@ struct ActorConfig {
     // are in flight at once (the GPU overlaps one batch's tail with the next,
     // DESIGN.md §3.2); at most 8
     uint32_t concurrent_reads = 0;
-    // A write segment applies all its removes, then all its adds.  The reference
-    // applies each replace as remove + add before the next message (usearch.rs:
-    // 214-221), so the key re-linked into a freed slot still sees every later key of
-    // the stream live.  Batching R replaces removes R rows at once, and the first of
-    // them are re-linked while the others are tombstones that may not be admitted as
-    // neighbours: self-recall after whole-index replace rounds drops from 0.999
-    // (sequential) to 0.98 at R = 256 and 0.87 at R = 3,000 of 3,000 keys (oracle,
-    // DESIGN.md §3.3a).  A segment therefore closes after live / replace_div removes
-    // (>= 1): at most 1/64 of the index is between its remove and its re-add
-    // (0: unbounded, round 5's first form; VSG_ACTOR_REPLACE_DIV overrides, probes).
-    size_t replace_div = 64;
+    // AddOrReplace runs go to the backend's replace in submission order (the
+    // reference's per-message remove + add, usearch.rs:214-221); `replace_batch` =
+    // keys per chunk (0: the index defaults, vsg_index_replace).  The chunks follow
+    // the keys and the index state, never the drain timing: an incomplete last
+    // chunk of a drained run is held back and re-submitted ahead of the next
+    // messages, applied at once when a barrier follows it (a Remove, or an Ann /
+    // Count / Flush in submission-order mode) and after hold_us without new writes
+    // (liveness; the only timing-dependent cut).  Round 5 cut a run into
+    // remove-all-then-add-all segments bounded to live / 64 removes at drain
+    // boundaries: self-recall 0.983-0.995 against 0.999 for the one-at-a-time
+    // sequence.
+    size_t replace_batch = 0;
+    uint32_t hold_us = 2000;
 };
 
 struct ActorCounters {
@@ -292,12 +318,27 @@ class Actor {
     // one worker: the FIFO of writes (and, by default, everything else), or the
     // Ann queue of concurrent_reads; both share qm_
     void run(std::deque<Msg>& q, std::condition_variable& cv) {
+        const bool writer = &q == &q_;
         std::vector<Msg> batch;
         for (;;) {
             {
                 std::unique_lock<std::mutex> lk(qm_);
-                cv.wait(lk, [&] { return stop_ || !q.empty(); });
-                if (q.empty() && stop_) return;
+                if (writer && !held_.empty()) {
+                    // a held chunk tail: apply it once the writes pause (liveness)
+                    if (!cv.wait_for(lk, std::chrono::microseconds(cfg_.hold_us),
+                                     [&] { return stop_ || !q.empty(); })) {
+                        lk.unlock();
+                        flush_held();
+                        continue;
+                    }
+                } else {
+                    cv.wait(lk, [&] { return stop_ || !q.empty(); });
+                }
+                if (q.empty() && stop_) {
+                    lk.unlock();
+                    if (writer) flush_held();
+                    return;
+                }
                 if (cfg_.max_wait_us && q.size() < cfg_.max_batch && !stop_) {
                     cv.wait_for(lk, std::chrono::microseconds(cfg_.max_wait_us),
                                 [&] { return stop_ || q.size() >= cfg_.max_batch; });
@@ -310,11 +351,11 @@ class Actor {
                     q.pop_front();
                 }
             }
-            process(batch);
+            process(batch, writer);
         }
     }
 
-    void process(std::vector<Msg>& b) {
+    void process(std::vector<Msg>& b, bool writer) {
         {
             std::lock_guard<std::mutex> lk(cm_);
             ctr_.messages += b.size();
@@ -324,8 +365,11 @@ class Actor {
             size_t j = i;
             if (b[i].kind == ADD || b[i].kind == REMOVE) {
                 while (j < b.size() && (b[j].kind == ADD || b[j].kind == REMOVE)) ++j;
-                writes(b, i, j);
+                writes(b, i, j, j == b.size());
                 maybe_compact();
+            } else if (writer && !held_.empty()) {
+                flush_held();  // a barrier: every earlier write applies first
+                continue;
             } else if (b[i].kind == ANN) {
                 while (j < b.size() && b[j].kind == ANN) ++j;
                 anns(b, i, j);
@@ -343,84 +387,82 @@ class Actor {
     }
 
     // ---------------------------------------------------------------- writes --
-    // A run of AddOrReplace / Remove messages in FIFO order becomes segments of
-    // one batched remove (keys to drop: explicit removes and the live key of a
-    // replace) followed by one batched add.  A key seen twice closes the
-    // segment, so every key's messages apply in order.
-    struct WriteSeg {
-        std::vector<uint64_t> rm, add;
-        std::vector<float> vecs;
-        std::unordered_set<uint64_t> touched;
-        std::vector<std::pair<AddDone, void*>> done;  // per add
-        void clear() {
-            rm.clear();
-            add.clear();
-            vecs.clear();
-            touched.clear();
-            done.clear();
-        }
-    };
-
-    void writes(std::vector<Msg>& b, size_t i0, size_t i1) {
-        WriteSeg s;
-        const size_t d = be_->dimensions();
+    // A run of AddOrReplace / Remove messages in FIFO order: each maximal run of
+    // AddOrReplace messages is one backend replace call (keys may repeat: the
+    // backend applies them in order), each run of Removes one remove call.  A held
+    // tail (held_) leads the next AddOrReplace run; may_hold: the run ends the
+    // drained batch (no barrier after it), so its incomplete last chunk may wait.
+    void writes(std::vector<Msg>& b, size_t i0, size_t i1, bool may_hold) {
         {
             std::lock_guard<std::mutex> lk(cm_);
             ctr_.writes += i1 - i0;
         }
-        size_t rm_cap = replace_cap();
-        for (size_t i = i0; i < i1; ++i) {
-            const Msg& m = b[i];
-            if (s.touched.count(m.key) || s.rm.size() >= rm_cap) {
-                apply(s);
-                rm_cap = replace_cap();
-            }
-            s.touched.insert(m.key);
-            if (m.kind == REMOVE) {
-                s.rm.push_back(m.key);
+        size_t i = i0;
+        while (i < i1) {
+            size_t j = i;
+            if (b[i].kind == REMOVE) {
+                flush_held();
+                std::vector<uint64_t> keys;
+                while (j < i1 && b[j].kind == REMOVE) keys.push_back(b[j++].key);
+                size_t removed = 0;
+                const int rc = be_->remove(keys.data(), keys.size(), &removed);
+                std::lock_guard<std::mutex> lk(cm_);
+                ctr_.remove_calls++;
+                if (rc) ctr_.remove_errors += keys.size();
             } else {
-                if (be_->contains(m.key)) s.rm.push_back(m.key);  // replace, usearch.rs:214-219
-                s.add.push_back(m.key);
-                s.vecs.insert(s.vecs.end(), m.vec.begin(), m.vec.begin() + d);
-                s.done.emplace_back(m.done, m.done_ctx);
+                while (j < i1 && b[j].kind == ADD) held_.push_back(std::move(b[j++]));
+                apply_held(may_hold && j == i1);
             }
+            i = j;
         }
-        apply(s);
     }
 
-    size_t replace_cap() const {  // replace_div 0: unbounded segments (probes)
-        return cfg_.replace_div ? std::max<size_t>(1, be_->size() / cfg_.replace_div) : SIZE_MAX;
+    void flush_held() {
+        if (!held_.empty()) apply_held(false);
     }
 
-    void apply(WriteSeg& s) {
-        if (!s.rm.empty()) {
-            size_t removed = 0;
-            const int rc = be_->remove(s.rm.data(), s.rm.size(), &removed);
+    // one replace call over the held AddOrReplace messages; with hold, the ones the
+    // backend left unapplied (status kHeld) stay held, in order
+    void apply_held(bool hold) {
+        const size_t n = held_.size();
+        if (n == 0) return;
+        const size_t d = be_->dimensions();
+        std::vector<uint64_t> keys(n);
+        std::vector<float> vecs(n * d);
+        for (size_t t = 0; t < n; ++t) {
+            keys[t] = held_[t].key;
+            std::memcpy(&vecs[t * d], held_[t].vec.data(), d * 4);
+        }
+        // usearch.rs:200-212 as if the run's vectors arrived one by one: the last one
+        // still finds free >= threshold before its add
+        int rc = 0;
+        while (rc == 0 && be_->capacity() - be_->size() < cfg_.reserve_threshold + n - 1) {
+            rc = be_->reserve(be_->capacity() + cfg_.reserve_increment);
             std::lock_guard<std::mutex> lk(cm_);
-            ctr_.remove_calls++;
-            if (rc) ctr_.remove_errors += s.rm.size();
+            ctr_.reserve_calls++;
         }
-        if (!s.add.empty()) {
-            // usearch.rs:200-212 as if the batch's vectors arrived one by one:
-            // the last one still finds free >= threshold before its add
-            int rc = 0;
-            const size_t n = s.add.size();
-            while (rc == 0 && be_->capacity() - be_->size() < cfg_.reserve_threshold + n - 1) {
-                rc = be_->reserve(be_->capacity() + cfg_.reserve_increment);
-                std::lock_guard<std::mutex> lk(cm_);
-                ctr_.reserve_calls++;
-            }
-            if (rc == 0) rc = be_->add(s.add.data(), s.vecs.data(), s.add.size());
-            {
-                std::lock_guard<std::mutex> lk(cm_);
-                ctr_.add_calls++;
-                ctr_.max_add_batch = std::max<uint64_t>(ctr_.max_add_batch, s.add.size());
-                if (rc) ctr_.add_errors += s.add.size();
-            }
-            for (size_t i = 0; i < n; ++i)
-                if (s.done[i].first) s.done[i].first(s.done[i].second, s.add[i], rc);
+        std::vector<int> status(n, rc);
+        if (rc == 0) be_->replace(keys.data(), vecs.data(), n, cfg_.replace_batch, hold, status.data());
+        size_t bad = 0, applied = 0;
+        for (int st : status) {
+            bad += st != 0 && st != ActorBackend::kHeld;
+            applied += st != ActorBackend::kHeld;
         }
-        s.clear();
+        {
+            std::lock_guard<std::mutex> lk(cm_);
+            if (applied) ctr_.add_calls++;
+            ctr_.max_add_batch = std::max<uint64_t>(ctr_.max_add_batch, applied);
+            ctr_.add_errors += bad;
+        }
+        std::vector<Msg> keep;
+        for (size_t t = 0; t < n; ++t) {
+            if (status[t] == ActorBackend::kHeld) {
+                keep.push_back(std::move(held_[t]));
+            } else if (held_[t].done) {
+                held_[t].done(held_[t].done_ctx, keys[t], status[t]);
+            }
+        }
+        held_.swap(keep);
     }
 
     void maybe_compact() {
@@ -504,6 +546,7 @@ class Actor {
                     else m.w->err = err;
                     m.w->finish(rc);
                 } else {  // ann_cb: the completion runs here, like a oneshot send
+                    if (rc) be_->set_error(err);  // an earlier completion may have overwritten it
                     m.ann_done(m.done_ctx, rc, c);
                 }
             }
@@ -522,6 +565,7 @@ class Actor {
     mutable std::mutex cm_;
     ActorCounters ctr_;
     std::atomic<uint64_t> wake_ns_{0};  // ann wake-up latency, summed (lock-free: every caller adds)
+    std::vector<Msg> held_;  // AddOrReplace messages of an incomplete chunk (writer only)
     std::thread worker_;
     std::vector<std::thread> readers_;
 };

@@ -141,8 +141,15 @@ __device__ void greedy_level(const GraphDev& g, const QReg<G, VM, T>& q, int l, 
 
 // Search-phase clocks (100 MHz wall clock), summed per wave into stats[10..13]
 // when built with -DVSG_SEARCH_PROFILE (tools only; zero cost otherwise).
+// The register beam also splits each expansion into shader-clock cycles
+// (s_memtime) summed into stats[20..31] (hnsw_search_reg.hip): picking the next
+// node, the adjacency-row wait, the visited-table inserts, the row-load wait and
+// the distance VALU of rows_dist, admission and compaction.
 struct BeamProf {
     uint64_t adj = 0, dist = 0, merge = 0;
+    uint64_t c_sel = 0, c_adj = 0, c_vis = 0, c_admit = 0, c_comp = 0, c_desc = 0;
+    uint32_t nexp = 0, ncomp = 0;
+    RowsProf rows;
 };
 #ifdef VSG_SEARCH_PROFILE
 #define VSG_CLK() wall_clock64()

@@ -243,8 +243,11 @@ template <int R> struct RegSet {
 };
 
 // Admit this lane's candidate key `ck` if `mine` (one expansion's batch).
+// pf: compaction cycles (the make prof build only).
 template <int R>
-__device__ __forceinline__ void admit(RegSet<R>& B, bool mine, uint64_t ck, bool lossy, int ef, uint64_t* sk) {
+__device__ __forceinline__ void admit(RegSet<R>& B, bool mine, uint64_t ck, bool lossy, int ef, uint64_t* sk,
+                                      BeamProf* pf = nullptr) {
+    (void)pf;
     const int lane = lane_id();
     bool valid = mine && ck < B.tkey;
     uint64_t vm = __ballot(valid);
@@ -258,10 +261,19 @@ __device__ __forceinline__ void admit(RegSet<R>& B, bool mine, uint64_t ck, bool
     }
     int nc = popc64(vm);
     if (nc && B.size + nc > 64 * R) {
+#ifdef VSG_SEARCH_PROFILE
+        const uint64_t tc = VSG_CYC();
+#endif
         B.compact(ef);
         valid = valid && ck < B.tkey;
         vm = __ballot(valid);
         nc = popc64(vm);
+#ifdef VSG_SEARCH_PROFILE
+        if (pf) {
+            pf->c_comp += VSG_CYC() - tc;
+            pf->ncomp++;
+        }
+#endif
     }
     if (nc) {
         if (valid) sk[lanes_below(vm)] = ck;
@@ -324,6 +336,7 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
     };
     for (;;) {
         const uint64_t t0 = VSG_CLK();
+        [[maybe_unused]] uint64_t c0c = VSG_CYC();
         const uint64_t a = B.min_unexpanded();
         if (a == VSG_KEY_EMPTY) break;
         if (B.size > ef && B.count_below(a) >= ef) break;
@@ -331,12 +344,27 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
         const uint32_t na = (uint32_t)a & VSG_ID_MASK;
         const uint32_t* row = row_of(na);
         ++nadj;
+#ifdef VSG_SEARCH_PROFILE
+        {
+            const uint64_t c = VSG_CYC();
+            pf.c_sel += c - c0c;
+            pf.nexp++;
+            c0c = c;
+        }
+#endif
         // one 64-entry piece of the row per pass (M0 = 2M <= 128); the expansion's
         // pieces are admitted one after another, which leaves the same set as one
         // batch (B only ever keeps the best ef of everything evaluated)
         for (int c0 = 0; c0 < m; c0 += 64) {
             const uint32_t nb = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
             const bool full = __ballot(nb != VSG_EMPTY) == ~0ull;
+#ifdef VSG_SEARCH_PROFILE
+            {
+                const uint64_t c = VSG_CYC();
+                pf.c_adj += c - c0c;
+                c0c = c;
+            }
+#endif
             bool fresh = false, evicted = false;
             if (nb != VSG_EMPTY && nb != self) fresh = w.vis.insert(nb, evicted);
             const uint64_t mask = __ballot(fresh);
@@ -346,14 +374,32 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
             wave_sync();
             const uint64_t t1 = VSG_CLK();
             pf.adj += t1 - t0;
+#ifdef VSG_SEARCH_PROFILE
+            {
+                const uint64_t c = VSG_CYC();
+                pf.c_vis += c - c0c;
+                c0c = c;
+            }
+#endif
             if (cnt) {
+#ifdef VSG_SEARCH_PROFILE
+                rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist, &pf.rows);
+#else
                 rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist);
+#endif
                 wave_sync();
                 ndist += (uint64_t)cnt;
                 const uint64_t ck = lane < cnt ? cand_key(w.tdist[lane], w.todo[lane]) : VSG_KEY_EMPTY;
                 const uint64_t t2 = VSG_CLK();
                 pf.dist += t2 - t1;
+#ifdef VSG_SEARCH_PROFILE
+                const uint64_t ca = VSG_CYC();
+                admit<R>(B, lane < cnt, ck, lossy, ef, sk, &pf);
+                c0c = VSG_CYC();
+                pf.c_admit += c0c - ca;
+#else
                 admit<R>(B, lane < cnt, ck, lossy, ef, sk);
+#endif
                 pf.merge += VSG_CLK() - t2;
             }
             if (!full) break;  // compact prefix: the row ended inside this piece

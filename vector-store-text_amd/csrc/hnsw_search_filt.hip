@@ -371,11 +371,14 @@ __global__ __launch_bounds__(64) void hnsw_search_filt_rerun_kernel(SearchParams
 }
 
 // One list per re-run block: 16 B x (slots + 64) entries; as many lists as fit
-// in 256 MiB (at least one, at most 16).
+// in 32 MiB (at least one, at most 16).  Every search workspace of an index with
+// removed entries carries them, for a re-run that is rare by design (ADVICE r5:
+// 256 MiB per workspace at 1M slots before); a workspace that cannot get them
+// searches in the degraded, counted mode instead of failing (vsg_index.cpp).
 void filt_rerun_shape(size_t slots, int* cap, int* nlists) {
     const size_t c = slots + 64;
     const size_t per = c * 16;
-    size_t nl = ((size_t)256 << 20) / per;
+    size_t nl = ((size_t)32 << 20) / per;
     nl = nl < 1 ? 1 : nl > 16 ? 16 : nl;
     *cap = (int)c;
     *nlists = (int)nl;

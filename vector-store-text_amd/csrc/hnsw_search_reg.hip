@@ -50,6 +50,7 @@ __device__ __forceinline__ void search_reg_one(const SearchParams& p, int qi, ui
     WaveLds w = carve(smem, 0, p.hash_size, 0);
     uint64_t ndist = 0, nadj = 0;
     BeamProf pf;
+    [[maybe_unused]] const uint64_t cq0 = VSG_CYC(), tq0 = VSG_CLK();
     int count = 0;
     uint64_t* ok = p.out_keys + (size_t)qi * p.k;
     float* od = p.out_dist + (size_t)qi * p.k;
@@ -74,7 +75,11 @@ __device__ __forceinline__ void search_reg_one(const SearchParams& p, int qi, ui
 #endif
             beam_reg<G, VM, U, T, MET, R>(g, q, 0, VSG_EMPTY, 0.f, p.ef, w, B, ndist, nadj, pf);
         } else {
+            [[maybe_unused]] const uint64_t cd0 = VSG_CYC();
             for (int l = p.max_level; l >= 1; --l) greedy_level<G, VM, U, T, MET>(g, q, l, cur, dcur, w, ndist, nadj);
+#ifdef VSG_SEARCH_PROFILE
+            pf.c_desc += VSG_CYC() - cd0;
+#endif
             beam_reg<G, VM, U, T, MET, R>(g, q, 0, cur, dcur, p.ef, w, B, ndist, nadj, pf);
         }
         // tombstones: skipped in the output, still traversed
@@ -124,6 +129,19 @@ __device__ __forceinline__ void search_reg_one(const SearchParams& p, int qi, ui
             atomicAdd(&p.stats[10], (unsigned long long)pf.adj);
             atomicAdd(&p.stats[11], (unsigned long long)pf.dist);
             atomicAdd(&p.stats[12], (unsigned long long)pf.merge);
+            // per-expansion breakdown, shader cycles (tools/gpu_probe.py --phases)
+            atomicAdd(&p.stats[20], (unsigned long long)pf.c_sel);
+            atomicAdd(&p.stats[21], (unsigned long long)pf.c_adj);
+            atomicAdd(&p.stats[22], (unsigned long long)pf.c_vis);
+            atomicAdd(&p.stats[23], (unsigned long long)pf.rows.wait);
+            atomicAdd(&p.stats[24], (unsigned long long)pf.rows.valu);
+            atomicAdd(&p.stats[25], (unsigned long long)pf.c_admit);
+            atomicAdd(&p.stats[26], (unsigned long long)pf.c_comp);
+            atomicAdd(&p.stats[27], (unsigned long long)pf.c_desc);
+            atomicAdd(&p.stats[28], (unsigned long long)pf.nexp | ((unsigned long long)pf.ncomp << 40));
+            atomicAdd(&p.stats[29], (unsigned long long)pf.rows.passes);
+            atomicAdd(&p.stats[30], (unsigned long long)(VSG_CYC() - cq0));
+            atomicAdd(&p.stats[31], (unsigned long long)(VSG_CLK() - tq0));
 #endif
         }
     }

@@ -32,6 +32,10 @@ struct IndexBackend final : vsg::ActorBackend {
     int reserve(size_t c) override { return vsg_index_reserve(h, c); }
     int add(const uint64_t* k, const float* v, size_t n) override { return vsg_index_add(h, k, v, n); }
     int remove(const uint64_t* k, size_t n, size_t* r) override { return vsg_index_remove(h, k, n, r); }
+    int replace(const uint64_t* k, const float* v, size_t n, size_t batch, bool hold, int* status) override {
+        return vsg_index_replace(h, k, v, n, batch, hold ? VSG_REPLACE_HOLD_TAIL : 0u, status, nullptr);
+    }
+    void set_error(const std::string& msg) override { vsg::set_last_error(msg); }
     int search(const float* q, size_t nq, size_t k, size_t e, uint64_t* keys, float* dist,
                size_t* counts) override {
         return vsg_index_search(h, q, nq, k, e, keys, dist, counts);
@@ -59,6 +63,10 @@ struct ShardedBackend final : vsg::ActorBackend {
     int reserve(size_t c) override { return vsg_sharded_reserve(h, c); }
     int add(const uint64_t* k, const float* v, size_t n) override { return vsg_sharded_add(h, k, v, n); }
     int remove(const uint64_t* k, size_t n, size_t* r) override { return vsg_sharded_remove(h, k, n, r); }
+    int replace(const uint64_t* k, const float* v, size_t n, size_t batch, bool hold, int* status) override {
+        return vsg_sharded_replace(h, k, v, n, batch, hold ? VSG_REPLACE_HOLD_TAIL : 0u, status, nullptr);
+    }
+    void set_error(const std::string& msg) override { vsg::set_last_error(msg); }
     int search(const float* q, size_t nq, size_t k, size_t e, uint64_t* keys, float* dist,
                size_t* counts) override {
         return vsg_sharded_search(h, q, nq, k, e, keys, dist, counts);
@@ -86,7 +94,10 @@ vsg::ActorConfig actor_config(const vsg_actor_options_t* o) {
     if (o->compact_percent) cfg.compact_percent = o->compact_percent;  // 0 => never (vsg.h)
     if (o->compact_min_dead) cfg.compact_min_dead = o->compact_min_dead;
     cfg.concurrent_reads = o->concurrent_reads;  // 0, 1, or n read workers (capped at 8)
-    if (const char* e = std::getenv("VSG_ACTOR_REPLACE_DIV")) cfg.replace_div = std::strtoull(e, nullptr, 10);
+    // keys per re-link chunk of a replace run (probes; 0 = the index default)
+    if (const char* e = std::getenv("VSG_ACTOR_REPLACE_BATCH")) cfg.replace_batch = std::strtoull(e, nullptr, 10);
+    // how long a held chunk tail waits for more writes (tests, probes)
+    if (const char* e = std::getenv("VSG_ACTOR_HOLD_US")) cfg.hold_us = (uint32_t)std::strtoul(e, nullptr, 10);
     return cfg;
 }
 

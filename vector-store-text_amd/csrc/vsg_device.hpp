@@ -239,15 +239,29 @@ __device__ __forceinline__ void mask_tail(uint4 (&raw)[VM], int nchunks, int sl)
 // before any arithmetic and kept as raw 16-B words (4 VGPRs each; f16 rows are
 // widened to f32 only when consumed), so the loads in flight cost half the
 // registers for f16 rows.
+// Search-profile clock (shader cycles, s_memtime; the make prof build only).
+#ifdef VSG_SEARCH_PROFILE
+#define VSG_CYC() __builtin_amdgcn_s_memtime()
+#else
+#define VSG_CYC() 0ull
+#endif
+// rows_dist's share of a profiled expansion: cycles waiting for the row loads
+// of each pass (an explicit vmcnt(0) after the pass is issued) and in its VALU.
+struct RowsProf {
+    uint64_t wait = 0, valu = 0;
+    uint32_t passes = 0;
+};
+
 template <int G, int VM, int U, typename T, int MET>
 __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size_t row_bytes,
                                           int nchunks, const uint32_t* ids, int count,
-                                          const QReg<G, VM, T>& q, float* out) {
+                                          const QReg<G, VM, T>& q, float* out, RowsProf* rp = nullptr) {
     constexpr int R = 64 / G;
     constexpr int E = ChunkT<T>::E;
     const int lane = lane_id();
     const int sub = lane / G;
     const int sl = lane % G;
+    (void)rp;
     for (int base = 0; base < count; base += R * U) {
         uint4 raw[U][VM];
 #pragma unroll
@@ -261,6 +275,17 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
                 raw[u][v] = *reinterpret_cast<const uint4*>(row + (size_t)(c < nchunks ? c : nchunks - 1) * 16);
             }
         }
+#ifdef VSG_SEARCH_PROFILE
+        uint64_t tp = 0;
+        if (rp) {
+            tp = VSG_CYC();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint64_t tw = VSG_CYC();
+            rp->wait += tw - tp;
+            rp->passes++;
+            tp = tw;
+        }
+#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             float acc = 0.f;
@@ -276,6 +301,9 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
             const int r = base + u * R + sub;
             if (sl == 0 && r < count) out[r] = (MET == MET_L2) ? acc : 1.f - acc;
         }
+#ifdef VSG_SEARCH_PROFILE
+        if (rp) rp->valu += VSG_CYC() - tp;
+#endif
     }
 }
 

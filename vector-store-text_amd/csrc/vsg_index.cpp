@@ -23,6 +23,7 @@
 #include <string>
 #include <system_error>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/vsg.h"
@@ -179,11 +180,20 @@ struct SearchCtx {
     uint8_t* dev = nullptr;  // device: queries | keys | dist | counts
     size_t dev_cap = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // VSG_PROFILE_HOST_SEARCH: H2D | kernels | D2H
+    // pipelined large calls (search_host): piece i's queries are in (pev[i], recorded
+    // on s by the upload) and its search + result copy run on ps[i] (ps[0] = s)
+    static constexpr int PIECES = 4;
+    hipStream_t ps[PIECES] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t pev[PIECES] = {nullptr, nullptr, nullptr, nullptr};
     ~SearchCtx() {
         if (pin) (void)hipHostFree(pin);
         if (dev) (void)hipFree(dev);
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : pev)
+            if (e) (void)hipEventDestroy(e);
+        for (int i = 1; i < PIECES; ++i)
+            if (ps[i]) (void)hipStreamDestroy(ps[i]);
         if (s) (void)hipStreamDestroy(s);
     }
 };
@@ -323,6 +333,7 @@ struct vsg_index {
     size_t reuse_cap = 0;  // slots
     int8_t* d_lvl_all = nullptr;  // every slot's level (edge-distance refresh)
     size_t lvl_all_cap = 0;
+    size_t lvl_all_rows = 0;  // d_lvl_all current for slots [0, lvl_all_rows)
     uint32_t entry = 0xFFFFFFFFu;
     int max_level = -1;
     std::atomic<uint64_t> build_vectors{0}, build_batches{0};
@@ -841,6 +852,7 @@ static uint8_t* staging(uint8_t* pinned, size_t cap, size_t need, std::vector<ui
 // table sized for them; upper_used is left to stage_slots.  add_common runs it
 // before any device work of the call: the table's growth synchronises the device.
 static int presize_slots(vsg_index* h, uint32_t s0, size_t n) {
+    h->lvl_all_rows = std::min(h->lvl_all_rows, (size_t)s0);  // levels of [s0, ...) rewritten
     int8_t* lv = h->h_levels.data() + s0;
     const uint32_t M = (uint32_t)h->M;
     const uint64_t seed = h->opt.seed;
@@ -864,6 +876,7 @@ static int stage_slots(vsg_index* h, uint32_t s0, size_t n, const uint64_t* keys
     uint32_t* upper_off = reinterpret_cast<uint32_t*>(kst + n);
     std::memcpy(kst, keys, n * 8);
     // levels and upper rows
+    h->lvl_all_rows = std::min(h->lvl_all_rows, (size_t)s0);
     size_t need_upper = h->upper_used;
     int8_t* lv = h->h_levels.data() + s0;
     const uint32_t M = (uint32_t)h->M;
@@ -898,12 +911,23 @@ static bool locality_on(const vsg_index* h, size_t n) {
            loc_row_floats(h) % 32 == 0 && n >= 2 * locality_min();
 }
 
+struct ReuseView;
+static hipError_t stage_reuse_batch(vsg_index* h, const ReuseView& v, size_t i0, size_t b, bool refresh,
+                                    hipStream_t st);
+static hipError_t finish_reuse_batch(vsg_index* h, const ReuseView& v, size_t i0, size_t b, hipStream_t st);
+static int ensure_lvl_all(vsg_index* h);
+
 // cells_done: add_common already enqueued compute_cells for these slots.
 // list: the call's reused slots (slot reuse: re-linked in place, n of them, in
-// this order before any appended slot; s0 is then the staged slot count, the
-// range an imported graph's edge distances are filled over); nullptr = the
-// appended range [s0, s0 + n).
-static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = false, const uint32_t* list = nullptr) {
+// this order -- the call's key order, batches are consecutive runs of it -- before
+// any appended slot; s0 is then the staged slot count, the range an imported
+// graph's edge distances are filled over); nullptr = the appended range
+// [s0, s0 + n).  rv: the reused slots' uploaded rows / keys / slots / levels
+// (list only), each batch staged from it right before its insert.
+// relink_batch (list only): nodes per re-link batch (0: the default rule below;
+// vsg_index_replace passes its chunk so one chunk is one batch).
+static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = false, const uint32_t* list = nullptr,
+                       const ReuseView* rv = nullptr, size_t relink_batch = 0) {
     hipStream_t st = h->stream;
     int rc;
     if (h->opt.flags & VSG_FLAG_EXACT_ONLY) {  // vectors only: no graph
@@ -958,13 +982,15 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
     pc.mark("b:cells_enqueue");
     const uint64_t pkey = host_splitmix64(h->opt.seed ^ 0x5045524D55544Eull ^ (uint64_t)s0);
     const SlotPerm perm(n, pkey);
-    if (pmode == 2) {
+    if (pmode == 2 && !list) {
         for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
         for (size_t i = n; i > 1; --i) std::swap(order[i - 1], order[(size_t)(host_splitmix64(pkey + i) % i)]);
     }
+    // a re-link pass keeps the call's order (a sequence of single adds; batch j
+    // is the reuse buffer's entries [B.i, B.i + B.b))
     host_parallel(n, [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {
-            const size_t li = pmode == 1 ? perm(i) : pmode == 2 ? order[i] : i;
+            const size_t li = list ? i : pmode == 1 ? perm(i) : pmode == 2 ? order[i] : i;
             order[i] = list ? list[li] : s0 + (uint32_t)li;
             blev[i] = h->h_levels[order[i]];
         }
@@ -1006,8 +1032,10 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
         std::max<size_t>(1, n / std::max<size_t>(1, (size_t)env_double("VSG_BUILD_MIN_BATCHES", minb_default)));
     // re-link pass (reused slots): a batch's reused nodes see each other's cleared
     // rows (dead ends) where the sequential update would see their new links, so the
-    // pass takes smaller batches -- at most graph / VSG_REUSE_BATCH_DIV nodes
-    const size_t rdiv = (size_t)env_double("VSG_REUSE_BATCH_DIV", 64);
+    // pass takes small batches -- at most graph / VSG_REUSE_BATCH_DIV nodes, the
+    // divisor vsg_index_replace's chunks use (round 5: 64, which left a 30k-row
+    // index's batched re-link 0.6-1 % below the one-key-at-a-time sequence)
+    const size_t rdiv = (size_t)env_double("VSG_REUSE_BATCH_DIV", 4096);
     // split insert (launch_insert_split): the efC beam at its own occupancy, then
     // the selection; lists of (node, level) in HBM between the two (VSG_BUILD_SPLIT=0:
     // the fused kernel; efC > 192 always fused)
@@ -1031,6 +1059,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
                                           (graph_nodes >= switch_at ? frac : frac_early));
             b = std::max<size_t>(1, std::min(std::min(b, bmax), bcall));
             if (list && rdiv > 1) b = std::max<size_t>(1, std::min(b, graph_nodes / rdiv));
+            if (list && relink_batch) b = std::min<size_t>(relink_batch, bmax);
             b = std::min(b, n - i);
             int new_top = -1;
             for (size_t j = i; j < i + b; ++j) {
@@ -1092,6 +1121,11 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
     HIP_TRY(hipMemcpyAsync(h->d_blevels, blev, n, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_pair_off, pair_off, n * 4, hipMemcpyHostToDevice, st));
     if (split) HIP_TRY(hipMemcpyAsync(h->d_list_off, list_off, n * 4, hipMemcpyHostToDevice, st));
+    // re-link pass: each batch's slots are staged right before it; the stored
+    // distances of links into them are refreshed when the graph has them
+    const bool refresh = list && edge_dist && h->adjd_valid;
+    if (list && !rv) return fail(VSG_EINVAL, "re-link pass without its reuse buffer");
+    if (refresh && (rc = ensure_lvl_all(h))) return rc;
     pc.mark("b:buffers+uploads");
 
     // pairs per reverse-kernel wave: with batches of up to 64k nodes, 64 pairs a
@@ -1107,6 +1141,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
         const Batch& B = plan[bi];
         // ev: insert start | insert end | sort end | reverse end | beam end (split)
         hipEvent_t* ev = &h->ev_pool[5 * bi];
+        if (list) HIP_TRY(stage_reuse_batch(h, *rv, B.i, B.b, refresh, st));
         HIP_TRY(hipMemsetAsync(h->d_pk[0], 0xFF, B.npairs * 8, st));
         InsertParams ip{};
         ip.g = h->graph(edge_dist);
@@ -1151,6 +1186,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
         const int grid = (int)std::max<size_t>(1, std::min<size_t>(rgrid, (B.npairs + ppw - 1) / ppw));
         HIP_TRY(launch_reverse(h->st, h->mk, rp, grid, st));
         HIP_TRY(hipEventRecord(ev[3], st));
+        if (list) HIP_TRY(finish_reuse_batch(h, *rv, B.i, B.b, st));
         if (B.new_top >= 0) {
             h->entry = B.top_node;
             h->max_level = B.new_top;
@@ -1471,12 +1507,14 @@ static ReuseView reuse_view(vsg_index* h, size_t r) {
     return v;
 }
 
-// Stage the reused slots (writer; mu held): keys / slots / levels uploaded, the
-// prepared rows scattered into their slots, every row of each slot cleared,
-// flags = removed | relink (searches keep skipping them until publish), then
-// the stored distances of links into them recomputed (adjd_valid graphs; an
-// imported graph gets all of its distances from build_slots' fill instead).
-static int stage_reuse(vsg_index* h, const uint64_t* keys, const std::vector<uint32_t>& slots) {
+// The reused slots of an add (writer; mu held): keys / slots / levels uploaded
+// once for the call.  Nothing in the graph changes here: each re-link batch is
+// staged right before its own insert launch (build_slots -> stage_reuse_batch),
+// so a slot later in the call keeps its old vector and links while earlier ones
+// are re-linked -- a multi-key add is a sequence of single adds, as usearch's
+// add_ pops one free slot per call (oracle orc_hnsw_add).  A failure here leaves
+// the graph and every flag untouched.
+static int upload_reuse(vsg_index* h, const uint64_t* keys, const std::vector<uint32_t>& slots) {
     const size_t r = slots.size();
     hipStream_t st = h->stream;
     ReuseView v = reuse_view(h, r);
@@ -1485,19 +1523,48 @@ static int stage_reuse(vsg_index* h, const uint64_t* keys, const std::vector<uin
     HIP_TRY(hipMemcpyAsync(v.keys, keys, r * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(v.slots, slots.data(), r * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(v.levels, lv.data(), r, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_reuse_stage(h->graph(h->d_adjd0 != nullptr), h->d_vecs, h->d_sqnorm, h->d_keys, h->d_flags, v.rows,
-                               v.sq, v.keys, v.slots, v.levels, r, st));
-    h->vec_gen++;  // rows rewritten in place: the f16 traversal copy is stale
-    const bool edge_dist = env_double("VSG_BUILD_EDGE_DIST", 1) != 0;
-    if (edge_dist && h->adjd_valid) {
-        int rc = ensure_buf(&h->d_lvl_all, h->lvl_all_cap, h->slots);
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(h->d_lvl_all, h->h_levels.data(), h->slots, hipMemcpyHostToDevice, st));
-        HIP_TRY(launch_edge_dist_refresh(h->st, h->mk, h->graph(true), h->d_lvl_all, h->d_flags, h->slots, st));
-    }
     // the uploads read pageable host memory (lv dies here)
     HIP_TRY(hipStreamSynchronize(st));
     return VSG_OK;
+}
+
+// every slot's level on the device (edge_dist_refresh_kernel): levels never
+// change for a stored slot, so only the slots staged since the last upload go up
+// (stage_slots / presize_slots / import lower lvl_all_rows when they rewrite any)
+static int ensure_lvl_all(vsg_index* h) {
+    if (h->slots > h->lvl_all_cap) {
+        int rc = ensure_buf(&h->d_lvl_all, h->lvl_all_cap, h->slots);
+        if (rc) return rc;
+        h->lvl_all_rows = 0;
+    }
+    if (h->lvl_all_rows < h->slots) {
+        HIP_TRY(hipMemcpyAsync(h->d_lvl_all + h->lvl_all_rows, h->h_levels.data() + h->lvl_all_rows,
+                               h->slots - h->lvl_all_rows, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));  // pageable source
+        h->lvl_all_rows = h->slots;
+    }
+    return VSG_OK;
+}
+
+// Stage reused slots [i0, i0 + b) of the call (build_slots, before that batch's
+// insert): prepared rows scattered into their slots, every row of each slot
+// cleared, flags = removed | relink (searches keep skipping them until publish;
+// the reverse kernel sees the relink bit), then the stored distances of links
+// into them recomputed (refresh: graphs with current stored distances).  After
+// the batch, finish_reuse_batch drops the relink bit again (removed only), so the
+// next batch's refresh also updates links that this batch's nodes made into the
+// slots staged next.
+static hipError_t stage_reuse_batch(vsg_index* h, const ReuseView& v, size_t i0, size_t b, bool refresh,
+                                    hipStream_t st) {
+    hipError_t e = launch_reuse_stage(h->graph(h->d_adjd0 != nullptr), h->d_vecs, h->d_sqnorm, h->d_keys, h->d_flags,
+                                      v.rows + i0 * h->row_bytes, v.sq + i0, v.keys + i0, v.slots + i0, v.levels + i0,
+                                      b, st);
+    if (e == hipSuccess && refresh)
+        e = launch_edge_dist_refresh(h->st, h->mk, h->graph(true), h->d_lvl_all, h->d_flags, h->slots, st);
+    return e;
+}
+static hipError_t finish_reuse_batch(vsg_index* h, const ReuseView& v, size_t i0, size_t b, hipStream_t st) {
+    return launch_set_flags(h->d_flags, v.slots + i0, b, 1, st);
 }
 
 // usearch::Index::add (src/index/usearch.rs:221), batched.  Stage under the
@@ -1506,11 +1573,11 @@ static int stage_reuse(vsg_index* h, const uint64_t* keys, const std::vector<uin
 // first keys take removed slots (the reference's replace is remove + add,
 // usearch.rs:214-221, and usearch re-links a removed slot on the next add);
 // see pick_free / stage_reuse and oracle orc_hnsw_add for the rules.
-static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, size_t n, bool device_src,
-                      hipStream_t user_stream) {
-    if (!h || (!keys && n) || (!vecs && n)) return fail(VSG_EINVAL, "null argument");
+// The writer lock (wmu) is held by the caller: add_common, or vsg_index_replace
+// across all of its chunks.  relink_batch: see build_slots.
+static int add_locked(vsg_index_t* h, const uint64_t* keys, const float* vecs, size_t n, bool device_src,
+                      hipStream_t user_stream, size_t relink_batch = 0) {
     if (n == 0) return VSG_OK;
-    std::lock_guard<std::mutex> wl(h->wmu);
     DeviceGuard dg(h->device);
     PhaseClock pc;
     int rc;
@@ -1581,23 +1648,25 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
         if (r) {
             ring_before = h->free_ring;
             take_free(h, reuse);
-            if ((rc = stage_reuse(h, keys, reuse))) {
-                // appended slots were staged: they become tombstones (ring), as after a failed build
+            if ((rc = upload_reuse(h, keys, reuse))) {
+                // appended slots were staged: they become tombstones (ring), as after a
+                // failed build; the reused slots were not touched (still removed, in the ring)
                 const std::string msg = g_last_error;
                 unmap_keys(h, keys, n);
                 h->free_ring = ring_before;
                 for (uint32_t s = s0; s < h->slots; ++s) h->free_ring.push_back(s);
                 (void)hipMemsetAsync(h->d_flags + s0, 1, h->slots - s0, h->stream);
-                if (h->d_reuse) (void)launch_set_flags(h->d_flags, reuse_view(h, r).slots, r, 1, h->stream);
                 (void)hipStreamSynchronize(h->stream);
                 publish(h);
                 g_last_error = msg;
                 return rc;
             }
+            h->vec_gen++;  // rows are rewritten in place by the build: the f16 traversal copy goes stale
         }
         pc.mark("stage");
     }
-    rc = r ? build_slots(h, (uint32_t)h->slots, r, false, reuse.data()) : VSG_OK;
+    const ReuseView rview = r ? reuse_view(h, r) : ReuseView{};
+    rc = r ? build_slots(h, (uint32_t)h->slots, r, false, reuse.data(), &rview, relink_batch) : VSG_OK;
     if (rc == VSG_OK && na) rc = build_slots(h, s0, na, cells);
     pc.mark("build_slots");
     if (rc == VSG_OK) {
@@ -1639,6 +1708,14 @@ static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
     return VSG_OK;
 }
 
+static int add_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, size_t n, bool device_src,
+                      hipStream_t user_stream) {
+    if (!h || (!keys && n) || (!vecs && n)) return fail(VSG_EINVAL, "null argument");
+    if (n == 0) return VSG_OK;
+    std::lock_guard<std::mutex> wl(h->wmu);
+    return add_locked(h, keys, vecs, n, device_src, user_stream);
+}
+
 int vsg_index_add(vsg_index_t* h, const uint64_t* keys, const float* vectors, size_t n) {
     VSG_RANGE();
     return add_common(h, keys, vectors, n, false, nullptr);
@@ -1650,10 +1727,8 @@ int vsg_index_add_device(vsg_index_t* h, const uint64_t* keys, const float* vect
     return add_common(h, keys, vectors_device, n, true, (hipStream_t)stream);
 }
 
-int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_removed) {
-    VSG_RANGE();
-    if (!h || (!keys && n)) return fail(VSG_EINVAL, "null argument");
-    std::lock_guard<std::mutex> wl(h->wmu);
+// wmu held by the caller (vsg_index_remove, vsg_index_replace)
+static int remove_locked(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_removed) {
     std::unique_lock<std::shared_mutex> lk(h->mu);
     DeviceGuard dg(h->device);
     // tombstone on the device first; the keys leave the map only once that
@@ -1682,6 +1757,118 @@ int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_r
     h->live -= removed;
     if (n_removed) *n_removed = removed;
     return VSG_OK;
+}
+
+int vsg_index_remove(vsg_index_t* h, const uint64_t* keys, size_t n, size_t* n_removed) {
+    VSG_RANGE();
+    if (!h || (!keys && n)) return fail(VSG_EINVAL, "null argument");
+    std::lock_guard<std::mutex> wl(h->wmu);
+    return remove_locked(h, keys, n, n_removed);
+}
+
+// The reference's AddOrReplace stream (src/index/usearch.rs:214-221: per message,
+// remove the live key, then add it, before the next message).  Sequential
+// semantics are kept key by key -- the slot each key takes is the one the
+// one-at-a-time sequence gives it (FIFO ring, entry point skipped) -- while the
+// keys are applied in chunks of consecutive messages: a chunk is one removal of
+// its live keys and one add, whose freed slots are re-linked as ONE batch.
+// Chunk sizes (batch = 0): keys re-linked into free slots, max(1, live /
+// VSG_REPLACE_DIV), 4096 by default -- at most 1/4096 of the index is between
+// its remove and its re-add, and below 8,192 live rows every key is its own chunk,
+// exactly the sequence; keys appended as new rows, max(1, live / 8), the bulk
+// build's rule (the add batches them >= 8 ways).  batch != 0 caps both.  A chunk
+// also ends at a repeated key (its second message must see the first applied) and
+// where the slot kind changes (re-linked / appended), so pick_free assigns each
+// key the slot of the sequence.  Chunk boundaries depend only on the keys and the
+// index state.  VSG_REPLACE_HOLD_TAIL: a last chunk that is not complete (fewer
+// keys than its size and nothing after it that ends it) is not applied --
+// its keys get status VSG_HELD, *n_applied counts the leading keys applied -- so a
+// caller feeding a stream in pieces (the actor) gets the same chunks however the
+// stream was cut.  Failures
+// are per chunk (status[]); the other chunks proceed, as the reference fails per
+// vector (usearch.rs:221-232).
+static int replace_common(vsg_index_t* h, const uint64_t* keys, const float* vecs, size_t n, size_t batch,
+                          uint32_t flags, int* status, size_t* n_applied, bool device_src, hipStream_t user_stream) {
+    if (n_applied) *n_applied = 0;
+    if (!h || (!keys && n) || (!vecs && n)) return fail(VSG_EINVAL, "null argument");
+    for (size_t i = 0; status && i < n; ++i) status[i] = VSG_OK;
+    if (n == 0) return VSG_OK;
+    std::lock_guard<std::mutex> wl(h->wmu);
+    DeviceGuard dg(h->device);
+    static const size_t div = std::max<size_t>(1, (size_t)env_double("VSG_REPLACE_DIV", 4096));
+    const bool hold = (flags & VSG_REPLACE_HOLD_TAIL) != 0;
+    int first = VSG_OK;
+    std::string first_msg;
+    auto record = [&](size_t lo, size_t hi, int rc) {
+        for (size_t t = lo; status && t < hi; ++t) status[t] = rc;
+        if (rc && !first) {
+            first = rc;
+            first_msg = g_last_error;
+        }
+    };
+    std::vector<uint64_t> rm;
+    std::unordered_set<uint64_t> seen;
+    size_t i = 0;
+    while (i < n) {
+        if (keys[i] >= KeyMap::DEAD) {
+            fail(VSG_EINVAL, "keys UINT64_MAX and UINT64_MAX-1 are reserved");
+            record(i, i + 1, VSG_EINVAL);
+            ++i;
+            continue;
+        }
+        size_t j = i, C = 1;
+        rm.clear();
+        seen.clear();
+        {
+            std::shared_lock<std::shared_mutex> lk(h->mu);  // wmu held: only searches run beside
+            const bool reuse = reuse_on(h);
+            size_t avail = h->free_ring.size();  // free slots an add may take (the entry's is skipped)
+            if (avail && std::find(h->free_ring.begin(), h->free_ring.end(), h->entry) != h->free_ring.end()) --avail;
+            int kind = -1;  // 1: the chunk's keys take free slots, 0: they are appended
+            for (; j < n; ++j) {
+                const uint64_t k = keys[j];
+                if (k >= KeyMap::DEAD || seen.count(k)) break;
+                uint32_t slot = 0;
+                const bool live = h->keys.find(k, &slot);
+                const size_t av = avail + (live && slot != h->entry ? 1 : 0);  // its remove frees a slot
+                const int kd = reuse && av > 0 ? 1 : 0;
+                if (kind < 0) {
+                    kind = kd;
+                    C = batch ? batch : std::max<size_t>(1, h->live / (kd ? div : 8));
+                } else if (kd != kind || j - i >= C) {
+                    break;
+                }
+                avail = av - (size_t)kd;
+                seen.insert(k);
+                if (live) rm.push_back(k);
+            }
+        }
+        // complete: full, or ended by the key after it; else the stream's tail
+        if (hold && j == n && j - i < C) {
+            for (size_t t = i; status && t < n; ++t) status[t] = VSG_HELD;
+            break;
+        }
+        int rc = rm.empty() ? VSG_OK : remove_locked(h, rm.data(), rm.size(), nullptr);
+        if (rc == VSG_OK)
+            rc = add_locked(h, keys + i, vecs + i * (size_t)h->dim, j - i, device_src, user_stream, j - i);
+        record(i, j, rc);
+        i = j;
+    }
+    if (n_applied) *n_applied = i;
+    if (first) g_last_error = first_msg;
+    return first;
+}
+
+int vsg_index_replace(vsg_index_t* h, const uint64_t* keys, const float* vectors, size_t n, size_t batch,
+                      uint32_t flags, int* status, size_t* n_applied) {
+    VSG_RANGE();
+    return replace_common(h, keys, vectors, n, batch, flags, status, n_applied, false, nullptr);
+}
+
+int vsg_index_replace_device(vsg_index_t* h, const uint64_t* keys, const float* vectors_device, size_t n,
+                             size_t batch, int* status, void* stream) {
+    VSG_RANGE();
+    return replace_common(h, keys, vectors_device, n, batch, 0, status, nullptr, true, (hipStream_t)stream);
 }
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1928,9 +2115,17 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
     // overflowing queries are re-run on device-memory lists (per-query flags +
     // the lists, hnsw_search_filt.hip)
     const bool filt = !exact && slots > h->live;
-    const size_t filt_b = filt ? align256(nq) + align256(filt_rerun_bytes(slots)) : 0;
+    bool rerun = filt && env_double("VSG_SEARCH_FILT_RERUN", 1) != 0;  // 0: degrade instead (probes)
+    size_t filt_b = filt ? align256(nq) + (rerun ? align256(filt_rerun_bytes(slots)) : 0) : 0;
     Workspace* ws = nullptr;
     int rc = ws_acquire(h, qp_b + qsq_b + 2 * part_b + rr_b + filt_b + 256, s, &ws);
+    if (rc && rerun) {
+        // no room for the re-run lists: the degraded, counted filtered search
+        // (search_filter_overflow) rather than a failed one
+        rerun = false;
+        filt_b = align256(nq);
+        rc = ws_acquire(h, qp_b + qsq_b + 2 * part_b + rr_b + filt_b + 256, s, &ws);
+    }
     if (rc) return rc;
     uint8_t* fb = ws->base + qp_b + qsq_b + 2 * part_b + rr_b;
     unsigned* qnext = reinterpret_cast<unsigned*>(fb + filt_b);  // persistent-grid counter (probes)
@@ -2047,11 +2242,16 @@ static int search_device_locked(vsg_index_t* h, const float* q_dev, size_t nq, s
         if (filt) {
             p.filt = 1;
             p.removed_frac = (float)((double)(slots - h->live) / (double)slots);
-            if (env_double("VSG_SEARCH_FILT_RERUN", 1) != 0) {  // 0: degrade instead (probes)
+            if (rerun) {
                 p.ovf = fb;
                 p.filt_lists = fb + align256(nq);
                 filt_rerun_shape(slots, &p.filt_cap, &p.filt_nlists);
             }
+            // the re-run kernel (sorted list in device memory) descends greedily, so
+            // the filtered search does too: an overflowing query gets the same walk
+            // as one that did not; multi-entry descent applies to
+            // indexes without removed entries
+            p.upper_ef = 0;
         }
         if (!rerank) {
             err = launch_search(h->st, h->mk, p, s);
@@ -2197,10 +2397,20 @@ static hipError_t copy_chunked(void* dst, const void* src, size_t bytes, hipMemc
 // as long as the search itself; 16 MiB pieces each copied by freshly started threads
 // still spent 1.35 ms in the upload (profiles/r05_host_search.jsonl).  Below 8 MiB (the
 // actor's batches) one memcpy and one transfer.
-static hipError_t h2d_staged(void* dst, uint8_t* pin, const void* src, size_t bytes, hipStream_t s) {
+// marks (optional, ascending byte offsets ending at `bytes`): mark_ev[j] is recorded on
+// s as soon as every byte below marks[j] has its DMA queued (search_host's pieces).
+static hipError_t h2d_staged(void* dst, uint8_t* pin, const void* src, size_t bytes, hipStream_t s,
+                             const size_t* marks = nullptr, size_t nmarks = 0, hipEvent_t* mark_ev = nullptr) {
+    size_t mj = 0;
+    auto record_marks = [&](size_t queued) {
+        hipError_t e = hipSuccess;
+        for (; mj < nmarks && marks[mj] <= queued && e == hipSuccess; ++mj) e = hipEventRecord(mark_ev[mj], s);
+        return e;
+    };
     if (bytes < ((size_t)8 << 20)) {
         std::memcpy(pin, src, bytes);
-        return copy_chunked(dst, pin, bytes, hipMemcpyHostToDevice, s);
+        hipError_t e = copy_chunked(dst, pin, bytes, hipMemcpyHostToDevice, s);
+        return e == hipSuccess ? record_marks(bytes) : e;
     }
     const size_t CH = (size_t)4 << 20;
     const size_t P = (bytes + CH - 1) / CH;
@@ -2226,7 +2436,8 @@ static hipError_t h2d_staged(void* dst, uint8_t* pin, const void* src, size_t by
     if (started < T - 1) {  // not all threads: copy everything here, then transfer
         for (auto& t : th) t.join();
         std::memcpy(pin, src, bytes);
-        return copy_chunked(dst, pin, bytes, hipMemcpyHostToDevice, s);
+        e = copy_chunked(dst, pin, bytes, hipMemcpyHostToDevice, s);
+        return e == hipSuccess ? record_marks(bytes) : e;
     }
     // this thread takes the last slice of every piece, then queues the piece
     for (size_t p = 0; p < P; ++p) {
@@ -2236,9 +2447,52 @@ static hipError_t h2d_staged(void* dst, uint8_t* pin, const void* src, size_t by
         done[p].fetch_add(1, std::memory_order_release);
         while (done[p].load(std::memory_order_acquire) < T) std::this_thread::yield();
         if (e == hipSuccess) e = hipMemcpyAsync(static_cast<uint8_t*>(dst) + off, pin + off, n, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = record_marks(off + n);
     }
     for (auto& t : th) t.join();
     return e;
+}
+
+// Large host-buffer calls in pieces: piece i's search starts as
+// soon as its queries landed, on its own stream (each takes its own scratch set, so
+// the pieces' kernels overlap on the device -- the next piece fills the previous
+// one's tail), and its results are copied back behind it; the upload of the pieces
+// after it runs under the search.  Same kernels and per-query results as one call.
+// VSG_HOST_SEARCH_PIECES: pieces (1 = one upload, one search, one download).
+static int search_host_pieces(vsg_index* h, SearchCtx* c, const float* queries, size_t nq, size_t k, size_t ef,
+                              bool exact, size_t P, uint8_t* dq, uint64_t* dk, float* dd, uint32_t* dc,
+                              uint8_t* pres) {
+    const size_t row = (size_t)h->dim * 4;
+    size_t marks[SearchCtx::PIECES];
+    for (size_t i = 0; i < P; ++i) {
+        marks[i] = (i + 1) * nq / P * row;
+        if (!c->pev[i]) HIP_TRY(hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming));
+        if (i && !c->ps[i]) HIP_TRY(hipStreamCreateWithFlags(&c->ps[i], hipStreamNonBlocking));
+    }
+    c->ps[0] = c->s;
+    if (h2d_staged(dq, c->pin, queries, nq * row, c->s, marks, P, c->pev) != hipSuccess)
+        return fail(VSG_EDEVICE, "H2D queries");
+    uint64_t* rk = reinterpret_cast<uint64_t*>(pres);
+    float* rd = reinterpret_cast<float*>(pres + align256(nq * k * 8));
+    uint32_t* rc_ = reinterpret_cast<uint32_t*>(pres + align256(nq * k * 8) + align256(nq * k * 4));
+    int rc = VSG_OK;
+    for (size_t i = 0; i < P && rc == VSG_OK; ++i) {
+        const size_t q0 = i * nq / P, q1 = (i + 1) * nq / P;
+        hipStream_t si = c->ps[i];
+        if (i) HIP_TRY(hipStreamWaitEvent(si, c->pev[i], 0));
+        rc = search_device_locked(h, reinterpret_cast<const float*>(dq + q0 * row), q1 - q0, k, ef, dk + q0 * k,
+                                  dd + q0 * k, dc + q0, si, exact);
+        if (rc) break;
+        if (hipMemcpyAsync(rk + q0 * k, dk + q0 * k, (q1 - q0) * k * 8, hipMemcpyDeviceToHost, si) != hipSuccess ||
+            hipMemcpyAsync(rd + q0 * k, dd + q0 * k, (q1 - q0) * k * 4, hipMemcpyDeviceToHost, si) != hipSuccess ||
+            hipMemcpyAsync(rc_ + q0, dc + q0, (q1 - q0) * 4, hipMemcpyDeviceToHost, si) != hipSuccess)
+            rc = fail(VSG_EDEVICE, "D2H results");
+    }
+    for (size_t i = 0; i < P; ++i) {  // every piece (also after a failure: the buffers are reused)
+        const hipError_t e = hipStreamSynchronize(c->ps[i]);
+        if (rc == VSG_OK && e != hipSuccess) rc = fail(VSG_EDEVICE, std::string("search: ") + hipGetErrorString(e));
+    }
+    return rc;
 }
 
 static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
@@ -2253,7 +2507,14 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
     if (!c) return fail(VSG_EDEVICE, "hipStreamCreate failed");
     const size_t qb = align256(nq * h->dim * 4), kb = align256(nq * k * 8), db = align256(nq * k * 4),
                  cb = align256(nq * 4);
-    int rc = ctx_reserve(c, std::max(qb, kb + db + cb), qb + kb + db + cb);
+    static const size_t max_pieces = std::min<size_t>(
+        SearchCtx::PIECES, std::max<size_t>(1, (size_t)env_double("VSG_HOST_SEARCH_PIECES", SearchCtx::PIECES)));
+    // pieces only where the upload is worth hiding (>= 16 MiB of queries, >= 1,024 per piece)
+    const size_t P = !exact && nq * h->dim * 4 >= ((size_t)16 << 20)
+                         ? std::min(max_pieces, std::max<size_t>(1, nq / 1024)) : 1;
+    // pinned: queries, then (pieces) a separate results area -- a piece's results come
+    // back while later pieces' queries are still being copied in
+    int rc = ctx_reserve(c, P > 1 ? qb + kb + db + cb : std::max(qb, kb + db + cb), qb + kb + db + cb);
     // device-timeline split of the call (VSG_PROFILE_HOST_SEARCH=1; tools/actor_load)
     static const bool prof = env_double("VSG_PROFILE_HOST_SEARCH", 0) != 0;
     if (rc == VSG_OK && prof && !c->ev[0])
@@ -2262,7 +2523,22 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
     auto mark = [&](int i) {
         if (prof && c->ev[i]) (void)hipEventRecord(c->ev[i], c->s);
     };
-    if (rc == VSG_OK) {
+    if (rc == VSG_OK && P > 1) {
+        uint8_t* dq = c->dev;
+        uint64_t* dk = reinterpret_cast<uint64_t*>(c->dev + qb);
+        float* dd = reinterpret_cast<float*>(c->dev + qb + kb);
+        uint32_t* dc = reinterpret_cast<uint32_t*>(c->dev + qb + kb + db);
+        uint8_t* pres = c->pin + qb;
+        rc = search_host_pieces(h, c, queries, nq, k, ef, exact, P, dq, dk, dd, dc, pres);
+        if (rc == VSG_OK) {
+            std::memcpy(out_keys, pres, nq * k * 8);
+            std::memcpy(out_dist, pres + kb, nq * k * 4);
+            if (out_counts) {
+                const uint32_t* cnt = reinterpret_cast<const uint32_t*>(pres + kb + db);
+                for (size_t i = 0; i < nq; ++i) out_counts[i] = cnt[i];
+            }
+        }
+    } else if (rc == VSG_OK) {
         uint8_t* dq = c->dev;
         uint64_t* dk = reinterpret_cast<uint64_t*>(c->dev + qb);
         float* dd = reinterpret_cast<float*>(c->dev + qb + kb);
@@ -2431,6 +2707,13 @@ extern "C" int vsg_debug_counters(const vsg_index_t* h, uint64_t* out16) {
     HIP_TRY(hipMemcpy(out16, h->d_stats, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return VSG_OK;
 }
+// the first n (<= 32) counters: [20..31] = the make prof search breakdown (hnsw_search_reg.hip)
+extern "C" int vsg_debug_counters_n(const vsg_index_t* h, uint64_t* out, size_t n) {
+    if (!h || !out || n > (size_t)VSG_NSTATS) return fail(VSG_EINVAL, "bad argument");
+    DeviceGuard dg(h->device);
+    HIP_TRY(hipMemcpy(out, h->d_stats, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return VSG_OK;
+}
 
 int vsg_index_reset_stats(vsg_index_t* h) {
     if (!h) return fail(VSG_EINVAL, "null index");
@@ -2549,6 +2832,7 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
     HIP_TRY(hipStreamSynchronize(st));
     hipFree(d);
     memcpy(h->h_levels.data(), levels, slots);
+    h->lvl_all_rows = 0;
     h->upper_used = upper_rows;
     h->slots = slots;
     h->live = 0;

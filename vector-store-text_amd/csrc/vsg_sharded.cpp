@@ -540,6 +540,42 @@ int vsg_sharded_add(vsg_sharded_t* h, const uint64_t* keys, const float* vectors
     return sfail(rc[bad], "shard " + std::to_string(bad) + ": " + msg[bad]);
 }
 
+// vsg_index_replace per shard: a key and all its messages meet on one shard
+// (route), so each shard applies its sub-stream in call order, all concurrently.
+int vsg_sharded_replace(vsg_sharded_t* h, const uint64_t* keys, const float* vectors, size_t n, size_t batch,
+                        uint32_t flags, int* status, size_t* n_applied) {
+    VSG_RANGE();
+    if (n_applied) *n_applied = 0;
+    if (!h || (n && (!keys || !vectors))) return sfail(VSG_EINVAL, "null argument");
+    for (size_t i = 0; status && i < n; ++i) status[i] = VSG_OK;
+    if (n == 0) return VSG_OK;
+    std::lock_guard<std::mutex> wl(h->wmu);
+    const size_t dim = h->opt.dimensions;
+    std::vector<std::vector<uint32_t>> rows(h->n);
+    for (size_t i = 0; i < n; ++i) rows[h->route(keys[i])].push_back((uint32_t)i);
+    std::vector<int> rc(h->n, VSG_OK);
+    std::vector<std::string> msg(h->n);
+    std::vector<size_t> applied(h->n, 0);
+    per_shard(h->n, [&](size_t g) {
+        const size_t ng = rows[g].size();
+        if (ng == 0) return;
+        std::vector<uint64_t> k(ng);
+        std::vector<float> v(ng * dim);
+        std::vector<int> st(ng, VSG_OK);
+        for (size_t j = 0; j < ng; ++j) {
+            k[j] = keys[rows[g][j]];
+            std::memcpy(&v[j * dim], vectors + (size_t)rows[g][j] * dim, dim * 4);
+        }
+        rc[g] = vsg_index_replace(h->shard[g], k.data(), v.data(), ng, batch, flags, st.data(), &applied[g]);
+        if (rc[g]) msg[g] = vsg_last_error();  // thread-local: read on this thread
+        for (size_t j = 0; status && j < ng; ++j) status[rows[g][j]] = st[j];
+    });
+    for (size_t g = 0; n_applied && g < h->n; ++g) *n_applied += applied[g];
+    for (size_t g = 0; g < h->n; ++g)
+        if (rc[g]) return sfail(rc[g], "shard " + std::to_string(g) + ": " + msg[g]);
+    return VSG_OK;
+}
+
 int vsg_sharded_remove(vsg_sharded_t* h, const uint64_t* keys, size_t n, size_t* n_removed) {
     VSG_RANGE();
     if (!h || (n && !keys)) return sfail(VSG_EINVAL, "null argument");

@@ -21,6 +21,8 @@ VSG_ENOMEM = 2
 VSG_EDUPKEY = 3
 VSG_EDEVICE = 4
 VSG_EUNSUPPORTED = 5
+VSG_HELD = 6  # vsg_index_replace status: left unapplied under VSG_REPLACE_HOLD_TAIL
+VSG_REPLACE_HOLD_TAIL = 1
 
 METRICS = {"l2sq": 0, "ip": 1, "cos": 2}
 SCALARS = {"f32": 0, "f16": 1}
@@ -165,6 +167,8 @@ def lib() -> C.CDLL:
         "vsg_index_add": (C.c_int, [P, P, P, sz]),
         "vsg_index_add_device": (C.c_int, [P, P, P, sz, P]),
         "vsg_index_remove": (C.c_int, [P, P, sz, C.POINTER(sz)]),
+        "vsg_index_replace": (C.c_int, [P, P, P, sz, sz, u32, P, C.POINTER(sz)]),
+        "vsg_index_replace_device": (C.c_int, [P, P, P, sz, sz, P, P]),
         "vsg_index_free_slots": (sz, [P, P, sz]),
         "vsg_index_search": (C.c_int, [P, P, sz, sz, sz, P, P, P]),
         "vsg_index_exact_search": (C.c_int, [P, P, sz, sz, P, P, P]),
@@ -211,6 +215,7 @@ def lib() -> C.CDLL:
         "vsg_sharded_shard": (P, [P, sz]),
         "vsg_sharded_add": (C.c_int, [P, P, P, sz]),
         "vsg_sharded_remove": (C.c_int, [P, P, sz, C.POINTER(sz)]),
+        "vsg_sharded_replace": (C.c_int, [P, P, P, sz, sz, u32, P, C.POINTER(sz)]),
         "vsg_sharded_search": (C.c_int, [P, P, sz, sz, sz, P, P, P]),
         "vsg_sharded_exact_search": (C.c_int, [P, P, sz, sz, P, P, P]),
         "vsg_sharded_search_device": (C.c_int, [P, P, sz, sz, sz, C.c_int, P, P, P]),

@@ -15,7 +15,7 @@ import numpy as np
 
 import os
 
-from ._lib import METRICS, NO_KEY, SCALARS, FileInfo, Options, Stats, check, lib
+from ._lib import METRICS, NO_KEY, SCALARS, VSG_REPLACE_HOLD_TAIL, FileInfo, Options, Stats, check, lib
 
 _METRIC_NAMES = {v: k for k, v in METRICS.items()}
 _SCALAR_NAMES = {v: k for k, v in SCALARS.items()}
@@ -110,6 +110,29 @@ class Index:
         n = C.c_size_t()
         check(lib().vsg_index_remove(self._h, _p(keys), len(keys), C.byref(n)))
         return n.value
+
+    def replace(self, keys, vectors, batch: int = 0, hold_tail: bool = False) -> np.ndarray:
+        """The reference's AddOrReplace stream (usearch.rs:214-221): per key in order,
+        remove it if live, then add it -- one-message-at-a-time results, applied by the
+        GPU in chunks (batch 0: max(1, size / 4096) keys re-linked, max(1, size / 8)
+        appended).  Returns the per-key status (0 = ok, VSG_HELD = left for the next
+        call under hold_tail); raises on the first error after the whole call ran."""
+        keys = np.ascontiguousarray(np.atleast_1d(keys), np.uint64)
+        vectors = np.ascontiguousarray(vectors, np.float32).reshape(len(keys), self.dimensions)
+        st = np.zeros(len(keys), np.int32)
+        na = C.c_size_t()
+        check(lib().vsg_index_replace(self._h, _p(keys), _p(vectors), len(keys), int(batch),
+                                      VSG_REPLACE_HOLD_TAIL if hold_tail else 0, _p(st), C.byref(na)))
+        return st
+
+    def replace_device(self, keys, vectors_t, batch: int = 0, stream=None) -> np.ndarray:
+        keys = np.ascontiguousarray(np.atleast_1d(keys), np.uint64)
+        assert vectors_t.is_cuda and vectors_t.is_contiguous()
+        assert vectors_t.shape == (len(keys), self.dimensions)
+        st = np.zeros(len(keys), np.int32)
+        check(lib().vsg_index_replace_device(self._h, _p(keys), _tp(vectors_t), len(keys), int(batch), _p(st),
+                                             _stream_ptr(stream)))
+        return st
 
     def free_slots(self) -> np.ndarray:
         """The free ring (usearch index_dense free_keys_): removed slots, oldest removal

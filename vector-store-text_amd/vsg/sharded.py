@@ -85,6 +85,16 @@ class ShardedIndex:
         check(lib().vsg_sharded_remove(self._h, _p(keys), len(keys), C.byref(n)))
         return n.value
 
+    def replace(self, keys, vectors, batch: int = 0) -> np.ndarray:
+        """vsg_index_replace on every shard (each key's messages meet on its shard)."""
+        keys = np.ascontiguousarray(np.atleast_1d(keys), np.uint64)
+        vectors = np.ascontiguousarray(vectors, np.float32).reshape(len(keys), self.dimensions)
+        st = np.zeros(len(keys), np.int32)
+        na = C.c_size_t()
+        check(lib().vsg_sharded_replace(self._h, _p(keys), _p(vectors), len(keys), int(batch), 0, _p(st),
+                                        C.byref(na)))
+        return st
+
     def _search(self, queries, k, ef, exact):
         q = np.ascontiguousarray(queries, np.float32).reshape(-1, self.dimensions)
         nq = q.shape[0]

@@ -72,11 +72,90 @@ struct DeviceGuard {
     }
 };
 
-template <typename X>
-hipError_t dev_alloc(X** p, size_t count) {
+// ------------------------------------------------------- device memory --
+// Stream-ordered device memory: every buffer an index owns
+// -- rows, graph, keys, build scratch, search workspaces -- comes from one
+// memory pool per device (hipMallocFromPoolAsync) and goes back to it with
+// hipFreeAsync on the index's own stream, after the host-side waits that cover
+// its readers (the index's stream, the device-search fence).  A plain hipFree
+// waits for the whole device, so freeing one index (or growing its capacity)
+// used to stall the freeing thread behind every other index's build and search.
+// The pool keeps what is freed (release threshold: all of it) for the next
+// allocation, as a caching allocator does; nothing is unmapped per free.
+hipMemPool_t device_pool(int dev) {
+    static std::mutex mu;
+    static std::vector<hipMemPool_t> pools;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((size_t)dev >= pools.size()) pools.resize((size_t)dev + 1, nullptr);
+    if (!pools[dev]) {
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t p = nullptr;
+        if (hipMemPoolCreate(&p, &props) != hipSuccess) return nullptr;
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+        pools[dev] = p;
+    }
+    return pools[dev];
+}
+
+hipError_t pool_alloc(void** p, size_t bytes, hipStream_t s) {
     *p = nullptr;
-    if (count == 0) count = 1;
-    return hipMalloc((void**)p, count * sizeof(X));
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipMemPool_t pool = device_pool(dev);
+    if (!pool) return hipErrorOutOfMemory;
+    return hipMallocFromPoolAsync(p, bytes ? bytes : 1, pool, s);
+}
+
+// stream-ordered free (nullptr: nothing); never a device-wide wait
+void dev_free(void* p, hipStream_t s) {
+    if (p) (void)hipFreeAsync(p, s);
+}
+
+template <typename X>
+hipError_t dev_alloc(X** p, size_t count, hipStream_t s) {
+    return pool_alloc((void**)p, (count ? count : 1) * sizeof(X), s);
+}
+
+// Pinned host staging, cached process-wide: hipHostFree waits for the device, so
+// buffers an index no longer needs go back here for the next one instead.
+struct PinnedCache {
+    std::mutex mu;
+    std::vector<std::pair<uint8_t*, size_t>> free[2];  // [coherent]
+};
+PinnedCache& pinned_cache() {
+    static PinnedCache* c = new PinnedCache;  // never destroyed (buffers outlive statics)
+    return *c;
+}
+hipError_t pinned_get(uint8_t** p, size_t* cap, size_t want, bool coherent) {
+    PinnedCache& c = pinned_cache();
+    {
+        std::lock_guard<std::mutex> lk(c.mu);
+        auto& v = c.free[coherent ? 1 : 0];
+        size_t best = v.size();
+        for (size_t i = 0; i < v.size(); ++i)
+            if (v[i].second >= want && (best == v.size() || v[i].second < v[best].second)) best = i;
+        if (best < v.size()) {
+            *p = v[best].first;
+            *cap = v[best].second;
+            v.erase(v.begin() + (long)best);
+            return hipSuccess;
+        }
+    }
+    *cap = 0;
+    const hipError_t e = hipHostMalloc((void**)p, want, coherent ? hipHostMallocCoherent : hipHostMallocDefault);
+    if (e == hipSuccess) *cap = want;
+    return e;
+}
+void pinned_put(uint8_t* p, size_t cap, bool coherent) {
+    if (!p) return;
+    PinnedCache& c = pinned_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.free[coherent ? 1 : 0].push_back({p, cap});
 }
 
 // level draw, bit-identical to oracle/vsg_oracle.c orc_sample_level
@@ -186,8 +265,9 @@ struct SearchCtx {
     hipStream_t ps[PIECES] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t pev[PIECES] = {nullptr, nullptr, nullptr, nullptr};
     ~SearchCtx() {
-        if (pin) (void)hipHostFree(pin);
-        if (dev) (void)hipFree(dev);
+        if (s) (void)hipStreamSynchronize(s);  // this context's own work only
+        pinned_put(pin, pin_cap, true);
+        dev_free(dev, s);
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : pev)
@@ -201,18 +281,20 @@ struct SearchCtx {
 // Device scratch of one search call (prepared queries, per-block partial
 // top-k lists).  Pooled per index and reused in stream order: a call on
 // stream S waits for the previous user's completion event before touching it.
-// (Stream-ordered hipMallocAsync blocks were not used: with the ROCm 7.2
-// runtime a reused >64 MiB block was seen to hold stale data past its first
-// 64 MiB while the next call's kernels ran -- tools/actor_load reproduces it.)
+// Its block comes from the device pool (allocated on the search's stream, freed
+// on the index's stream after the last search using it completed).  (Round 4
+// saw a reused >64 MiB block hold stale data past its first 64 MiB; the cause
+// was one >64 MiB hipMemcpyAsync completing out of order -- copy_chunked.)
 struct Workspace {
     uint8_t* base = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;
     bool pending = false;
     hipStream_t last = nullptr;  // stream of the last search that used it
+    hipStream_t home = nullptr;  // the index's stream: frees are ordered on it
     ~Workspace() {
         if (pending) (void)hipEventSynchronize(done);
-        if (base) (void)hipFree(base);
+        dev_free(base, home);
         if (done) (void)hipEventDestroy(done);
     }
 };
@@ -358,10 +440,6 @@ struct vsg_index {
     uint32_t* d_pv[2] = {nullptr, nullptr};
     size_t pairs_cap = 0;
     void* d_sort_tmp = nullptr;
-    // build scratch outgrown during an add: freed once the add's stream drained
-    // (hipFree synchronises the device, which would stall the host's planning
-    // until the locality cells enqueued just before had finished)
-    std::vector<void*> defer_free;
     // pinned host staging of an add's plan (insertion order, levels, pair and
     // list offsets): pageable hipMemcpyAsync blocks the host until the stream
     // reaches the copy, i.e. until the locality cells enqueued before it ran
@@ -429,14 +507,15 @@ struct vsg_index {
     }
 };
 
-static void flush_deferred(vsg_index* h);
-
+// Everything the index owns goes back: device buffers to the pool, ordered on
+// the index's stream (the caller drained the device-search fence and the stream's
+// own work), pinned staging to the process-wide cache -- no device-wide wait.
 static void free_dev(vsg_index* h) {
-    flush_deferred(h);  // hipFree waits for the device
-    if (h->h_plan) (void)hipHostFree(h->h_plan);
+    hipStream_t st = h->stream;
+    pinned_put(h->h_plan, h->h_plan_cap, false);
     h->h_plan = nullptr;
     h->h_plan_cap = 0;
-    if (h->h_stg) (void)hipHostFree(h->h_stg);
+    pinned_put(h->h_stg, h->h_stg_cap, false);
     h->h_stg = nullptr;
     h->h_stg_cap = 0;
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
@@ -446,44 +525,16 @@ static void free_dev(vsg_index* h) {
     for (Workspace* w : h->ws_free) delete w;
     h->ws_count -= std::min(h->ws_count, h->ws_free.size());
     h->ws_free.clear();
-    hipFree(h->d_rm);
-    hipFree(h->d_reuse);
-    hipFree(h->d_lvl_all);
-    hipFree(h->d_vecs);
-    hipFree(h->d_vecs16);
-    hipFree(h->d_ktile);
-    hipFree(h->d_adj0);
-    hipFree(h->d_upper_off);
-    hipFree(h->d_upper);
-    hipFree(h->d_adjd0);
-    hipFree(h->d_upperd);
-    hipFree(h->d_keys);
-    hipFree(h->d_flags);
-    hipFree(h->d_sqnorm);
-    hipFree(h->d_stats);
-    hipFree(h->d_blevels);
-    hipFree(h->d_pair_off);
-    hipFree(h->d_bnodes);
-    hipFree(h->d_list_off);
-    hipFree(h->d_lst_d);
-    hipFree(h->d_lst_i);
-    hipFree(h->d_lst_n);
-    for (int i = 0; i < 2; ++i) {
-        hipFree(h->d_pk[i]);
-        hipFree(h->d_pv[i]);
-    }
-    hipFree(h->d_sort_tmp);
-    hipFree(h->d_stage);
-    hipFree(h->d_piv);
-    hipFree(h->d_pivbf);
-    hipFree(h->d_cell);
-    hipFree(h->d_cf32);
-    hipFree(h->d_cpart_d);
-    hipFree(h->d_cpart_i);
-    for (int i = 0; i < 2; ++i) {
-        hipFree(h->d_okey[i]);
-        hipFree(h->d_oidx[i]);
-    }
+    for (void* p : {(void*)h->d_rm, (void*)h->d_reuse, (void*)h->d_lvl_all, (void*)h->d_vecs, (void*)h->d_vecs16,
+                    (void*)h->d_ktile, (void*)h->d_adj0, (void*)h->d_upper_off, (void*)h->d_upper,
+                    (void*)h->d_adjd0, (void*)h->d_upperd, (void*)h->d_keys, (void*)h->d_flags,
+                    (void*)h->d_sqnorm, (void*)h->d_stats, (void*)h->d_blevels, (void*)h->d_pair_off,
+                    (void*)h->d_bnodes, (void*)h->d_list_off, (void*)h->d_lst_d, (void*)h->d_lst_i,
+                    (void*)h->d_lst_n, (void*)h->d_pk[0], (void*)h->d_pk[1], (void*)h->d_pv[0], (void*)h->d_pv[1],
+                    h->d_sort_tmp, (void*)h->d_stage, (void*)h->d_piv, (void*)h->d_pivbf, (void*)h->d_cell,
+                    (void*)h->d_cf32, (void*)h->d_cpart_d, (void*)h->d_cpart_i, (void*)h->d_okey[0],
+                    (void*)h->d_okey[1], (void*)h->d_oidx[0], (void*)h->d_oidx[1]})
+        dev_free(p, st);
 }
 
 
@@ -491,11 +542,12 @@ static void free_dev(vsg_index* h) {
 template <typename X>
 static int grow_array(X** arr, size_t used, size_t newcap, int fill, hipStream_t s) {
     X* n = nullptr;
-    HIP_TRY(dev_alloc(&n, newcap));
+    HIP_TRY(dev_alloc(&n, newcap, s));
     if (used && *arr) HIP_TRY(hipMemcpyAsync(n, *arr, used * sizeof(X), hipMemcpyDeviceToDevice, s));
     if (newcap > used) HIP_TRY(hipMemsetAsync(n + used, fill, (newcap - used) * sizeof(X), s));
+    // the index's own stream only: searches on other streams read the new array next
     HIP_TRY(hipStreamSynchronize(s));
-    hipFree(*arr);
+    dev_free(*arr, s);
     *arr = n;
     return VSG_OK;
 }
@@ -506,10 +558,10 @@ static int reserve_locked(vsg_index* h, size_t capacity) {
     h->fence.drain();  // enqueued device searches read the arrays freed below
     const size_t s = h->slots;
     uint8_t* nv = nullptr;
-    HIP_TRY(dev_alloc(&nv, capacity * h->row_bytes));
+    HIP_TRY(dev_alloc(&nv, capacity * h->row_bytes, h->stream));
     if (s) HIP_TRY(hipMemcpyAsync(nv, h->d_vecs, s * h->row_bytes, hipMemcpyDeviceToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
-    hipFree(h->d_vecs);
+    dev_free(h->d_vecs, h->stream);
     h->d_vecs = nv;
     h->vec_gen++;
     int rc;
@@ -540,25 +592,25 @@ static int ensure_upper(vsg_index* h, size_t rows) {
     return VSG_OK;
 }
 
+// a writer-side buffer of the index, regrown on its stream (contents not kept)
 template <typename X>
-static int ensure_buf(X** p, size_t& cap, size_t need) {
+static int ensure_buf(X** p, size_t& cap, size_t need, hipStream_t s) {
     if (need <= cap) return VSG_OK;
     size_t want = std::max(need, cap * 2);
-    hipFree(*p);
+    dev_free(*p, s);
     *p = nullptr;
-    HIP_TRY(dev_alloc(p, want));
+    cap = 0;
+    HIP_TRY(dev_alloc(p, want, s));
     cap = want;
     return VSG_OK;
 }
 
-// release a build scratch buffer after the add's device work (flush_deferred)
+// release an outgrown build scratch buffer, ordered after the add's device work
+// already queued on the index's stream (round 4 deferred a hipFree to the end of
+// the add: it synchronised the device)
 template <typename X> static void dfree(vsg_index* h, X*& p) {
-    if (p) h->defer_free.push_back((void*)p);
+    dev_free((void*)p, h->stream);
     p = nullptr;
-}
-static void flush_deferred(vsg_index* h) {
-    for (void* p : h->defer_free) (void)hipFree(p);
-    h->defer_free.clear();
 }
 
 // per-add node buffers (levels, pair offsets) and per-batch pair buffers
@@ -570,10 +622,10 @@ static int ensure_nodes(vsg_index* h, size_t n) {
     dfree(h, h->d_bnodes);
     dfree(h, h->d_list_off);
     h->bnodes_cap = 0;
-    HIP_TRY(dev_alloc(&h->d_blevels, want));
-    HIP_TRY(dev_alloc(&h->d_pair_off, want));
-    HIP_TRY(dev_alloc(&h->d_bnodes, want));
-    HIP_TRY(dev_alloc(&h->d_list_off, want));
+    HIP_TRY(dev_alloc(&h->d_blevels, want, h->stream));
+    HIP_TRY(dev_alloc(&h->d_pair_off, want, h->stream));
+    HIP_TRY(dev_alloc(&h->d_bnodes, want, h->stream));
+    HIP_TRY(dev_alloc(&h->d_list_off, want, h->stream));
     h->bnodes_cap = want;
     return VSG_OK;
 }
@@ -585,9 +637,9 @@ static int ensure_lists(vsg_index* h, size_t lists) {
     dfree(h, h->d_lst_i);
     dfree(h, h->d_lst_n);
     h->lst_cap = 0;
-    HIP_TRY(dev_alloc(&h->d_lst_d, want * (size_t)h->efc));
-    HIP_TRY(dev_alloc(&h->d_lst_i, want * (size_t)h->efc));
-    HIP_TRY(dev_alloc(&h->d_lst_n, want));
+    HIP_TRY(dev_alloc(&h->d_lst_d, want * (size_t)h->efc, h->stream));
+    HIP_TRY(dev_alloc(&h->d_lst_i, want * (size_t)h->efc, h->stream));
+    HIP_TRY(dev_alloc(&h->d_lst_n, want, h->stream));
     h->lst_cap = want;
     return VSG_OK;
 }
@@ -618,27 +670,27 @@ static size_t loc_chunk(const vsg_index* h, size_t n) {
 
 static int ensure_locality(vsg_index* h, size_t n, size_t max_b, size_t part_entries, size_t chunk = 0) {
     const size_t rf = loc_row_floats(h);
-    if (!h->d_piv) HIP_TRY(dev_alloc(&h->d_piv, LOC_PIVOTS * (rf * 4 + 4 + 1 + 4 + 8) + 256));
-    if (!h->d_pivbf) HIP_TRY(dev_alloc(&h->d_pivbf, cells_pivot_bytes((int)LOC_PIVOTS, (int)rf)));
+    if (!h->d_piv) HIP_TRY(dev_alloc(&h->d_piv, LOC_PIVOTS * (rf * 4 + 4 + 1 + 4 + 8) + 256, h->stream));
+    if (!h->d_pivbf) HIP_TRY(dev_alloc(&h->d_pivbf, cells_pivot_bytes((int)LOC_PIVOTS, (int)rf), h->stream));
     if (h->st == ST_F16 && chunk > h->cf32_cap) {
         dfree(h, h->d_cf32);
         h->cf32_cap = 0;
-        HIP_TRY(dev_alloc(&h->d_cf32, chunk * rf));
+        HIP_TRY(dev_alloc(&h->d_cf32, chunk * rf, h->stream));
         h->cf32_cap = chunk;
     }
     if (n > h->cell_cap) {
         const size_t want = std::max(n, h->cell_cap * 2);
         dfree(h, h->d_cell);
         h->cell_cap = 0;
-        HIP_TRY(dev_alloc(&h->d_cell, want));
+        HIP_TRY(dev_alloc(&h->d_cell, want, h->stream));
         h->cell_cap = want;
     }
     if (part_entries > h->cpart_cap) {
         dfree(h, h->d_cpart_d);
         dfree(h, h->d_cpart_i);
         h->cpart_cap = 0;
-        HIP_TRY(dev_alloc(&h->d_cpart_d, part_entries));
-        HIP_TRY(dev_alloc(&h->d_cpart_i, part_entries));
+        HIP_TRY(dev_alloc(&h->d_cpart_d, part_entries, h->stream));
+        HIP_TRY(dev_alloc(&h->d_cpart_i, part_entries, h->stream));
         h->cpart_cap = part_entries;
     }
     if (max_b > h->border_cap) {
@@ -648,8 +700,8 @@ static int ensure_locality(vsg_index* h, size_t n, size_t max_b, size_t part_ent
         }
         h->border_cap = 0;
         for (int i = 0; i < 2; ++i) {
-            HIP_TRY(dev_alloc(&h->d_okey[i], max_b));
-            HIP_TRY(dev_alloc(&h->d_oidx[i], max_b));
+            HIP_TRY(dev_alloc(&h->d_okey[i], max_b, h->stream));
+            HIP_TRY(dev_alloc(&h->d_oidx[i], max_b, h->stream));
         }
         h->border_cap = max_b;
     }
@@ -788,8 +840,8 @@ static int ensure_pairs(vsg_index* h, size_t n) {
     }
     h->pairs_cap = 0;
     for (int i = 0; i < 2; ++i) {
-        HIP_TRY(dev_alloc(&h->d_pk[i], want));
-        HIP_TRY(dev_alloc(&h->d_pv[i], want));
+        HIP_TRY(dev_alloc(&h->d_pk[i], want, h->stream));
+        HIP_TRY(dev_alloc(&h->d_pv[i], want, h->stream));
     }
     h->pairs_cap = want;
     return VSG_OK;
@@ -835,11 +887,10 @@ static int ensure_pinned(uint8_t** p, size_t& cap, size_t need) {
     const size_t pmax = pin_max();
     if (need <= cap || need > pmax) return VSG_OK;
     const size_t want = std::min(pmax, std::max(need, cap * 2));
-    if (*p) (void)hipHostFree(*p);
+    pinned_put(*p, cap, false);  // its copies completed: the previous call synchronised
     *p = nullptr;
     cap = 0;
-    HIP_TRY(hipHostMalloc((void**)p, want, hipHostMallocDefault));
-    cap = want;
+    HIP_TRY(pinned_get(p, &cap, want, false));
     return VSG_OK;
 }
 static uint8_t* staging(uint8_t* pinned, size_t cap, size_t need, std::vector<uint8_t>& fallback) {
@@ -948,13 +999,13 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
             if (h->upper_used > 0 && !h->d_upperd)
                 return fail(VSG_EDEVICE, "edge distances: upper rows without a distance table");
             int8_t* dl = nullptr;
-            HIP_TRY(dev_alloc(&dl, s0));
+            HIP_TRY(dev_alloc(&dl, s0, st));
             // dl freed on every path (the launch and sync may fail)
             hipError_t e = hipMemcpyAsync(dl, h->h_levels.data(), s0, hipMemcpyHostToDevice, st);
             if (e == hipSuccess) e = launch_edge_dist_fill(h->st, h->mk, h->graph(true), dl, s0, st);
             const hipError_t es = hipStreamSynchronize(st);
             if (e == hipSuccess) e = es;
-            hipFree(dl);
+            dev_free(dl, st);
             if (e != hipSuccess) return fail(VSG_EDEVICE, std::string("edge distances: ") + hipGetErrorString(e));
         }
         h->adjd_valid = true;
@@ -1108,7 +1159,7 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
         if (tmp > h->sort_tmp_bytes) {
             dfree(h, h->d_sort_tmp);
             h->sort_tmp_bytes = 0;
-            HIP_TRY(hipMalloc(&h->d_sort_tmp, tmp * 2));
+            HIP_TRY(pool_alloc(&h->d_sort_tmp, tmp * 2, st));
             h->sort_tmp_bytes = tmp * 2;
         }
     }
@@ -1200,7 +1251,6 @@ static int build_slots(vsg_index* h, uint32_t s0, size_t n, bool cells_done = fa
     pc.mark("b:enqueue_batches");
     if (!plan.empty()) {
         HIP_TRY(hipStreamSynchronize(st));
-        flush_deferred(h);
         pc.mark("b:device_drain");
         // VSG_DEBUG_TIMING=2: one line per batch (probes)
         const bool per_batch = env_double("VSG_DEBUG_TIMING", 0) >= 2;
@@ -1377,8 +1427,9 @@ int vsg_index_new(const vsg_index_options_t* o, vsg_index_t** out) {
         delete h;
         return fail(VSG_EDEVICE, "hipStreamCreate failed");
     }
-    if (hipMalloc(&h->d_stats, VSG_NSTATS * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(h->d_stats, 0, VSG_NSTATS * sizeof(unsigned long long)) != hipSuccess) {
+    if (dev_alloc(&h->d_stats, VSG_NSTATS, h->stream) != hipSuccess ||
+        hipMemsetAsync(h->d_stats, 0, VSG_NSTATS * sizeof(unsigned long long), h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess) {
         delete h;
         return fail(VSG_ENOMEM, "stats allocation failed");
     }
@@ -1390,7 +1441,10 @@ void vsg_index_free(vsg_index_t* h) {
     VSG_RANGE();
     if (!h) return;
     {
+        // this index's own work only (its stream, its enqueued device searches):
+        // the buffers go back to the pool in stream order, no device-wide wait
         DeviceGuard dg(h->device);
+        h->fence.drain();
         hipStreamSynchronize(h->stream);
         free_dev(h);
         hipStreamDestroy(h->stream);
@@ -1436,7 +1490,7 @@ static int put_rows(vsg_index_t* h, const float* vecs, size_t n, bool device_src
         HIP_TRY(launch_prepare(h->st, vecs, n, h->dim, h->normalize, dst, h->row_bytes, h->stream, dst_sq));
     } else {
         const size_t chunk = 65536;
-        if ((rc = ensure_buf(&h->d_stage, h->stage_cap, std::min(n, chunk) * h->dim))) return rc;
+        if ((rc = ensure_buf(&h->d_stage, h->stage_cap, std::min(n, chunk) * h->dim, h->stream))) return rc;
         for (size_t off = 0; off < n; off += chunk) {
             const size_t c = std::min(chunk, n - off);
             HIP_TRY(hipMemcpyAsync(h->d_stage, vecs + off * h->dim, c * h->dim * 4, hipMemcpyHostToDevice, h->stream));
@@ -1533,7 +1587,7 @@ static int upload_reuse(vsg_index* h, const uint64_t* keys, const std::vector<ui
 // (stage_slots / presize_slots / import lower lvl_all_rows when they rewrite any)
 static int ensure_lvl_all(vsg_index* h) {
     if (h->slots > h->lvl_all_cap) {
-        int rc = ensure_buf(&h->d_lvl_all, h->lvl_all_cap, h->slots);
+        int rc = ensure_buf(&h->d_lvl_all, h->lvl_all_cap, h->slots, h->stream);
         if (rc) return rc;
         h->lvl_all_rows = 0;
     }
@@ -1612,11 +1666,10 @@ static int add_locked(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
         return rc;
     if (r) {  // the reused slots' rows go to a staging buffer (scattered by stage_reuse)
         if (r > h->reuse_cap) {
-            flush_deferred(h);
-            hipFree(h->d_reuse);
+            dev_free(h->d_reuse, h->stream);
             h->d_reuse = nullptr;
             h->reuse_cap = 0;
-            HIP_TRY(dev_alloc(&h->d_reuse, reuse_bytes(h, r)));
+            HIP_TRY(dev_alloc(&h->d_reuse, reuse_bytes(h, r), h->stream));
             h->reuse_cap = r;
         }
         const ReuseView v = reuse_view(h, r);
@@ -1742,7 +1795,7 @@ static int remove_locked(vsg_index_t* h, const uint64_t* keys, size_t n, size_t*
         hit.push_back(keys[i]);
     }
     if (!slots.empty()) {
-        int rc = ensure_buf(&h->d_rm, h->rm_cap, slots.size());
+        int rc = ensure_buf(&h->d_rm, h->rm_cap, slots.size(), h->stream);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(h->d_rm, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, h->stream));
         HIP_TRY(launch_set_flags(h->d_flags, h->d_rm, slots.size(), 1, h->stream));
@@ -1918,6 +1971,7 @@ static int ws_acquire(vsg_index* h, size_t bytes, hipStream_t s, Workspace** out
     };
     if (!w) {
         w = new Workspace;
+        w->home = h->stream;
         if (hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess) {
             drop(w);
             return fail(VSG_EDEVICE, "hipEventCreate failed");
@@ -1926,11 +1980,11 @@ static int ws_acquire(vsg_index* h, size_t bytes, hipStream_t s, Workspace** out
     if (w->cap < bytes) {
         if (w->pending) (void)hipEventSynchronize(w->done);
         w->pending = false;
-        if (w->base) (void)hipFree(w->base);
+        dev_free(w->base, h->stream);  // its last search completed (event above)
         w->base = nullptr;
         const size_t want = std::max(bytes, w->cap * 2);
         w->cap = 0;
-        if (hipMalloc((void**)&w->base, want) != hipSuccess) {
+        if (pool_alloc((void**)&w->base, want, s) != hipSuccess) {
             drop(w);
             return fail(VSG_ENOMEM, "search workspace");
         }
@@ -1963,10 +2017,10 @@ static int ensure_shadow(vsg_index* h, hipStream_t s) {
     if (h->shadow_gen != h->vec_gen || h->shadow_cap < slots || h->shadow_rows > slots) {
         if (h->shadow_cap < h->cap) {
             h->fence.drain();  // device searches enqueued earlier may walk the old copy
-            hipFree(h->d_vecs16);
+            dev_free(h->d_vecs16, s);
             h->d_vecs16 = nullptr;
             h->shadow_cap = 0;
-            HIP_TRY(dev_alloc(&h->d_vecs16, h->cap * h->row_bytes16));
+            HIP_TRY(dev_alloc(&h->d_vecs16, h->cap * h->row_bytes16, h->stream));
             h->shadow_cap = h->cap;
         }
         // zeros past the published rows: a search beside a build may reach rows of
@@ -2007,10 +2061,10 @@ static int ensure_ktile(vsg_index* h, size_t slots, hipStream_t s) {
     if (h->ktile_gen != h->vec_gen || h->ktile_cap < want_cap || h->ktile_rows > slots) {
         if (h->ktile_cap < want_cap) {
             h->fence.drain();
-            hipFree(h->d_ktile);
+            dev_free(h->d_ktile, s);
             h->d_ktile = nullptr;
             h->ktile_cap = 0;
-            HIP_TRY(dev_alloc(&h->d_ktile, want_cap * (h->row_bytes / 4)));
+            HIP_TRY(dev_alloc(&h->d_ktile, want_cap * (h->row_bytes / 4), h->stream));
             // padding rows of the last tile are read (clamped loads never, but keep them defined)
             HIP_TRY(hipMemsetAsync(h->d_ktile, 0, want_cap * h->row_bytes, s));
             h->ktile_cap = want_cap;
@@ -2355,21 +2409,20 @@ static void ctx_release(vsg_index* h, SearchCtx* c) {
 static int ctx_reserve(SearchCtx* c, size_t pin_bytes, size_t dev_bytes) {
     if (pin_bytes > c->pin_cap) {
         const size_t want = std::max(pin_bytes, c->pin_cap * 2);  // before the old capacity is cleared
-        if (c->pin) HIP_TRY(hipHostFree(c->pin));
+        pinned_put(c->pin, c->pin_cap, true);  // the context's calls all synchronised
         c->pin = nullptr;
         c->pin_cap = 0;
         // coherent (snooped) pinned memory: the buffer is written and read by
         // the CPU around the DMA; a non-coherent mapping lets the copy engine
         // read lines still dirty in the CPU caches (seen as stale query rows)
-        HIP_TRY(hipHostMalloc((void**)&c->pin, want, hipHostMallocCoherent));
-        c->pin_cap = want;
+        HIP_TRY(pinned_get(&c->pin, &c->pin_cap, want, true));
     }
     if (dev_bytes > c->dev_cap) {
         const size_t want = std::max(dev_bytes, c->dev_cap * 2);
-        if (c->dev) HIP_TRY(hipFree(c->dev));
+        dev_free(c->dev, c->s);
         c->dev = nullptr;
         c->dev_cap = 0;
-        HIP_TRY(hipMalloc((void**)&c->dev, want));
+        HIP_TRY(pool_alloc((void**)&c->dev, want, c->s));
         c->dev_cap = want;
     }
     return VSG_OK;
@@ -2604,8 +2657,8 @@ int vsg_index_set_f16_traversal(vsg_index_t* h, int enable) {
     h->f16_trav = enable != 0;
     h->opt.flags = enable ? (h->opt.flags | VSG_FLAG_F16_TRAVERSAL) : (h->opt.flags & ~VSG_FLAG_F16_TRAVERSAL);
     if (!enable && h->d_vecs16) {
-        HIP_TRY(hipDeviceSynchronize());
-        hipFree(h->d_vecs16);
+        h->fence.drain();  // device searches enqueued earlier may still walk the copy (mu held:
+        dev_free(h->d_vecs16, h->stream);  // no host search is in flight)
         h->d_vecs16 = nullptr;
         h->shadow_cap = h->shadow_rows = 0;
         h->shadow_gen = ~0ull;
@@ -2769,11 +2822,12 @@ int vsg_index_export(const vsg_index_t* h, float* vectors, uint64_t* keys, uint8
     hipStream_t st = h->stream;
     if (vectors && s) {
         float* d = nullptr;
-        HIP_TRY(hipMalloc(&d, s * h->dim * 4));
-        HIP_TRY(launch_unprepare(h->st, h->d_vecs, s, h->dim, h->row_bytes, d, st));
-        HIP_TRY(hipMemcpyAsync(vectors, d, s * h->dim * 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        hipFree(d);
+        HIP_TRY(dev_alloc(&d, s * h->dim, st));
+        hipError_t e = launch_unprepare(h->st, h->d_vecs, s, h->dim, h->row_bytes, d, st);
+        if (e == hipSuccess) e = copy_chunked(vectors, d, s * h->dim * 4, hipMemcpyDeviceToHost, st);
+        const hipError_t es = hipStreamSynchronize(st);
+        dev_free(d, st);
+        HIP_TRY(e != hipSuccess ? e : es);
     }
     if (keys && s) HIP_TRY(hipMemcpyAsync(keys, h->d_keys, s * 8, hipMemcpyDeviceToHost, st));
     if (removed && s) HIP_TRY(hipMemcpyAsync(removed, h->d_flags, s, hipMemcpyDeviceToHost, st));
@@ -2820,7 +2874,7 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
     if ((rc = ensure_upper(h, upper_rows))) return rc;
     hipStream_t st = h->stream;
     float* d = nullptr;
-    HIP_TRY(hipMalloc(&d, slots * h->dim * 4));
+    HIP_TRY(dev_alloc(&d, slots * h->dim, st));
     HIP_TRY(hipMemcpyAsync(d, vectors, slots * h->dim * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(launch_prepare(h->st, d, slots, h->dim, h->normalize, h->d_vecs, h->row_bytes, st, h->d_sqnorm));
     h->vec_gen++;
@@ -2830,7 +2884,7 @@ int vsg_index_import(vsg_index_t* h, size_t slots, const float* vectors, const u
     HIP_TRY(hipMemcpyAsync(h->d_upper_off, upper_off, slots * 4, hipMemcpyHostToDevice, st));
     if (upper_rows) HIP_TRY(hipMemcpyAsync(h->d_upper, upper, upper_rows * h->M * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));
-    hipFree(d);
+    dev_free(d, st);
     memcpy(h->h_levels.data(), levels, slots);
     h->lvl_all_rows = 0;
     h->upper_used = upper_rows;
@@ -2883,13 +2937,13 @@ int vsg_index_compact(vsg_index_t* h, size_t* n_dropped) {
     float* nsq = nullptr;
     uint64_t* nk = nullptr;
     auto release = [&]() {
-        hipFree(d_idx);
-        hipFree(nv);
-        hipFree(nsq);
-        hipFree(nk);
+        dev_free(d_idx, st);
+        dev_free(nv, st);
+        dev_free(nsq, st);
+        dev_free(nk, st);
     };
-    if (n && (dev_alloc(&d_idx, n) != hipSuccess || dev_alloc(&nv, n * h->row_bytes) != hipSuccess ||
-              dev_alloc(&nsq, n) != hipSuccess || dev_alloc(&nk, n) != hipSuccess)) {
+    if (n && (dev_alloc(&d_idx, n, st) != hipSuccess || dev_alloc(&nv, n * h->row_bytes, st) != hipSuccess ||
+              dev_alloc(&nsq, n, st) != hipSuccess || dev_alloc(&nk, n, st) != hipSuccess)) {
         release();
         return fail(VSG_ENOMEM, "compaction scratch");
     }

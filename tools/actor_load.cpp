@@ -12,7 +12,7 @@
 //         completions (vsg_actor_ann_cb, the reference's oneshot reply): each finished
 //         query submits that client's next one from its callback -- no thread per client]
 //        [seed: the index's level seed (bench.py passes its own, so the graph is the
-//         headline index's)]
+//         headline index's)] [max_batch: anns per worker drain, 0 = the actor default]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -51,6 +51,7 @@ int main(int argc, char** argv) {
     const unsigned readers = argc > 9 ? (unsigned)std::atoi(argv[9]) : 0;
     const int mode = argc > 10 ? std::atoi(argv[10]) : 0;
     const uint64_t index_seed = argc > 11 ? std::strtoull(argv[11], nullptr, 0) : 1;
+    const unsigned max_batch = argc > 12 ? (unsigned)std::atoi(argv[12]) : 0;
     const uint64_t cfg = 2, base_seed = 0x5EED0000 + cfg, q_seed = 0x5EED1000 + cfg, m_seed = 0x5EED2000 + cfg;
 
     vsg_actor_options_t o{};
@@ -61,6 +62,7 @@ int main(int argc, char** argv) {
     o.index.expansion_search = (uint32_t)ef;
     o.index.seed = index_seed;
     o.max_wait_us = wait_us;
+    o.max_batch = max_batch;
     o.concurrent_reads = readers;
     vsg_actor_t* a = nullptr;
     TRY(vsg_actor_new(&o, &a));
@@ -249,10 +251,10 @@ int main(int argc, char** argv) {
                  (s1.host_device_ns - s0.host_device_ns) / 1e3 / hs, (s1.host_d2h_ns - s0.host_d2h_ns) / 1e3 / hs);
     std::printf(
         "{\"rows\": %zu, \"dim\": %zu, \"clients\": %d, \"queries\": %zu, \"k\": %zu, \"ef\": %zu, "
-        "\"max_wait_us\": %u, \"read_workers\": %u, \"clients_as\": \"%s\", \"actor_qps\": %.1f, \"batched_qps\": %.1f, \"lat_us_p50\": %.1f, "
+        "\"max_wait_us\": %u, \"max_batch\": %u, \"read_workers\": %u, \"clients_as\": \"%s\", \"actor_qps\": %.1f, \"batched_qps\": %.1f, \"lat_us_p50\": %.1f, "
         "\"lat_us_p99\": %.1f, \"search_calls\": %llu, \"mean_batch\": %.1f, \"max_batch\": %llu, "
         "\"mismatch_vs_batched\": %d, \"errors\": %d}\n",
-        rows, dim, clients, nq, k, ef, wait_us, readers, mode == 1 ? "completions" : "threads", nq / served_s, nq / batched_s, lat[nq / 2], lat[nq * 99 / 100],
+        rows, dim, clients, nq, k, ef, wait_us, max_batch, readers, mode == 1 ? "completions" : "threads", nq / served_s, nq / batched_s, lat[nq / 2], lat[nq * 99 / 100],
         (unsigned long long)calls, calls ? (double)nq / calls : 0.0, (unsigned long long)c1.max_search_batch,
         mismatch.load(), errors.load());
     vsg_actor_free(a);

@@ -308,6 +308,7 @@ class Actor {
     void push(Msg&& m) {
         m.t_enq = steady_ns();
         const bool read = cfg_.concurrent_reads > 0 && m.kind == ANN;
+        if (read) inflight_.fetch_add(1, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> lk(qm_);
             (read ? rq_ : q_).push_back(std::move(m));
@@ -339,17 +340,34 @@ class Actor {
                     if (writer) flush_held();
                     return;
                 }
-                if (cfg_.max_wait_us && q.size() < cfg_.max_batch && !stop_) {
+                size_t cap = cfg_.max_batch;
+                if (!writer && cfg_.concurrent_reads >= 2) {
+                    // Two or more read workers split the anns in flight evenly, so that as
+                    // many search batches overlap on the device: a worker takes its share
+                    // -- ceil(anns in flight / workers), in flight = queued or being searched
+                    // -- waiting up to the coalescing window (max_wait_us, else 300 us) for
+                    // it to be queued.  Closed-loop clients then form one group per worker,
+                    // each group's next batch filling while the other groups' run (round 5:
+                    // one batch of all the clients at a time, the device idle between them).
+                    const size_t readers = cfg_.concurrent_reads;
+                    const size_t share = std::max<size_t>(
+                        1, (inflight_.load(std::memory_order_relaxed) + readers - 1) / readers);
+                    cap = std::min(cap, share);
+                    const uint32_t win = cfg_.max_wait_us ? cfg_.max_wait_us : 300;
+                    if (q.size() < cap && !stop_)
+                        cv.wait_for(lk, std::chrono::microseconds(win), [&] { return stop_ || q.size() >= cap; });
+                } else if (cfg_.max_wait_us && q.size() < cfg_.max_batch && !stop_) {
                     cv.wait_for(lk, std::chrono::microseconds(cfg_.max_wait_us),
                                 [&] { return stop_ || q.size() >= cfg_.max_batch; });
                 }
-                const size_t n = std::min(q.size(), cfg_.max_batch);
+                const size_t n = std::min(q.size(), cap);
                 batch.clear();
                 batch.reserve(n);
                 for (size_t i = 0; i < n; ++i) {
                     batch.push_back(std::move(q.front()));
                     q.pop_front();
                 }
+                if (!writer && !q.empty()) cv.notify_one();  // the rest: another read worker
             }
             process(batch, writer);
         }
@@ -549,6 +567,7 @@ class Actor {
                     if (rc) be_->set_error(err);  // an earlier completion may have overwritten it
                     m.ann_done(m.done_ctx, rc, c);
                 }
+                if (cfg_.concurrent_reads > 0) inflight_.fetch_sub(1, std::memory_order_relaxed);
             }
             const uint64_t dn = steady_ns() - tn;
             std::lock_guard<std::mutex> lk(cm_);
@@ -565,6 +584,7 @@ class Actor {
     mutable std::mutex cm_;
     ActorCounters ctr_;
     std::atomic<uint64_t> wake_ns_{0};  // ann wake-up latency, summed (lock-free: every caller adds)
+    std::atomic<size_t> inflight_{0};   // anns on the read queue or in a search (concurrent_reads)
     std::vector<Msg> held_;  // AddOrReplace messages of an incomplete chunk (writer only)
     std::thread worker_;
     std::vector<std::thread> readers_;

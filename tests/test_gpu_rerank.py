@@ -70,6 +70,30 @@ def test_rerank_tracks_appends_removals_and_compaction():
     _same(b.search(q, 16, 80), a.search(q, 16, 80))
 
 
+def test_rerank_tracks_replaced_rows():
+    """Replaces re-link freed slots in place (vsg_index_replace): the f16 copy gets exactly
+    the rewritten rows re-converted (not the whole copy), and the f16 walk + re-rank still
+    equals the f32 walk bit for bit on integer data -- after replace calls of one key and of
+    many, with the copy built before them."""
+    dim, nq, n = 64, 150, 8000
+    x = G.uint8_valued(n + 3000, dim, 91)
+    q = G.uint8_valued(nq, dim, 92)
+    a = vsg.Index(dim, "l2sq", "f32", 16, 64, 40, seed=6)
+    b = vsg.Index(dim, "l2sq", "f32", 16, 64, 40, seed=6, f16_traversal=True)
+    a.add(np.arange(n), x[:n])
+    b.add(np.arange(n), x[:n])
+    _same(b.search(q, 10, 48), a.search(q, 10, 48))  # the copy exists before the replaces
+    rng = np.random.default_rng(4)
+    row = n
+    for batch in (1, 40, 700):
+        keys = rng.choice(n, batch, replace=False).astype(np.uint64)
+        assert (a.replace(keys, x[row:row + batch]) == 0).all()
+        assert (b.replace(keys, x[row:row + batch]) == 0).all()
+        row += batch
+        _same(b.search(q, 10, 48), a.search(q, 10, 48))
+    assert b.graph_info()["slots"] <= n + 1
+
+
 def test_rerank_after_compacting_everything():
     """Every row removed, compaction drops all of them (slots -> 0), different rows
     re-added: the f16 copy must be rebuilt, not reused."""

@@ -15,10 +15,13 @@ for v in prof base; do
   [ "$v" = prof ] && lib=vector-store-text_amd/lib_prof/libvsg.so && ph="--phases"
   for nq in 512 10000; do
     VSG_LIB_PATH=$lib timeout -k 10 240 python3 -u tools/gpu_probe.py search --queries $nq --gt-queries $nq \
-      --efs 36 --steps 5 $ph | sed "s/^{/{\"lib\": \"$v\", \"cfg\": \"c2\", /" >> $out 2>> gpurun_out/r06_phases.err || exit 1
+      --efs 36 --steps 5 $ph \
+      | sed "s/^{/{\"lib\": \"$v\", \"cfg\": \"c2\", /" >> $out 2>> gpurun_out/r06_phases.err || exit 1
   done
+  # register rows: 4 (default at ef 192) / 8 / 17 -- same results, fewer compactions
   VSG_LIB_PATH=$lib timeout -k 10 300 python3 -u tools/gpu_probe.py search --rows 100000000 --shards 8 --shard 0 \
     --dim 128 --quant f16 --metric l2sq --data sift --config 3 --queries 10000 --gt-queries 1000 --efs 64,192 \
-    --steps 3 $ph | sed "s/^{/{\"lib\": \"$v\", \"cfg\": \"c4shard\", /" >> $out 2>> gpurun_out/r06_phases.err || exit 1
+    --steps 3 $ph --set "" --set VSG_SEARCH_REG_ROWS=8 --set VSG_SEARCH_REG_ROWS=17 \
+    | sed "s/^{/{\"lib\": \"$v\", \"cfg\": \"c4shard\", /" >> $out 2>> gpurun_out/r06_phases.err || exit 1
 done
 echo done

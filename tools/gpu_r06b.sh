@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 900 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu \
-  tests/test_gpu_slot_reuse.py tests/test_gpu_actor.py tests/test_gpu_usearch_semantics.py tests/test_gpu_multi_entry.py tests/test_gpu_concurrency.py \
+  tests/test_gpu_slot_reuse.py tests/test_gpu_actor.py tests/test_gpu_usearch_semantics.py tests/test_gpu_multi_entry.py tests/test_gpu_concurrency.py tests/test_gpu_rerank.py \
   > gpurun_out/r06b_tests.log 2>&1 || { tail -30 gpurun_out/r06b_tests.log; exit 1; }
 tail -3 gpurun_out/r06b_tests.log
 timeout -k 10 1000 python3 -u -m pytest -x -v -s --timeout 900 --timeout-method thread -m gpu tests/test_gpu_c2_parity.py \

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Round 6: serving through the actor at C2 (tools/actor_load, closed-loop clients of
 # single-query vsg_actor_ann_cb, ef 36): one read worker (round 5's configuration) vs
-# two / four read workers with batches capped at clients / workers and a coalescing
-# window -- two batches in flight, each half of the clients.
+# two / four read workers splitting the anns in flight evenly (one batch per worker on
+# the device at once; coalescing window 300 us, or 150).
 # gpurun_out/r06_actor.jsonl
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -16,9 +16,10 @@ run() {  # clients wait_us readers max_batch
   grep breakdown gpurun_out/r06_actor_run.err | sed "s/^/# c$1 w$2 r$3 b$4 /" >> gpurun_out/r06_actor_breakdown.txt || true
 }
 run 512 0 1 0
-run 512 0 2 256
-run 512 150 2 256
-run 512 150 4 128
+run 512 0 2 0
+run 512 0 4 0
+run 512 150 2 0
 run 2048 0 1 0
-run 2048 150 2 1024
+run 2048 0 2 0
+run 2048 0 4 0
 echo done

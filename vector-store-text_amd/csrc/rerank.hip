@@ -111,4 +111,36 @@ hipError_t launch_shadow_f16(const uint8_t* vecs, size_t row_bytes, size_t r0, s
     return hipGetLastError();
 }
 
+// the f16 copy of listed rows only (rows rewritten in place by a slot-reusing add)
+__global__ __launch_bounds__(256) void shadow_f16_slots_kernel(const uint8_t* __restrict__ vecs, size_t row_bytes,
+                                                               const uint32_t* __restrict__ slots, size_t n,
+                                                               size_t limit, int dim, uint8_t* __restrict__ out,
+                                                               size_t row_bytes16) {
+    const size_t nc = row_bytes16 / 16;
+    const size_t tot = n * nc;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = slots[i / nc];
+        if (r >= limit) continue;  // beyond the converted rows: the next incremental pass covers it
+        const int c = (int)(i % nc);
+        const float* src = reinterpret_cast<const float*>(vecs + r * row_bytes);
+        half8_t h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int j = c * 8 + e;
+            h[e] = (_Float16)(j < dim ? src[j] : 0.f);
+        }
+        *reinterpret_cast<uint4*>(out + r * row_bytes16 + (size_t)c * 16) = __builtin_bit_cast(uint4, h);
+    }
+}
+
+hipError_t launch_shadow_f16_slots(const uint8_t* vecs, size_t row_bytes, const uint32_t* slots, size_t n,
+                                   size_t limit, int dim, uint8_t* out, size_t row_bytes16, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const size_t tot = n * (row_bytes16 / 16);
+    const unsigned grid = (unsigned)std::min<size_t>((tot + 255) / 256, 1u << 20);
+    hipLaunchKernelGGL(shadow_f16_slots_kernel, dim3(grid), dim3(256), 0, s, vecs, row_bytes, slots, n, limit, dim,
+                       out, row_bytes16);
+    return hipGetLastError();
+}
+
 }  // namespace vsg

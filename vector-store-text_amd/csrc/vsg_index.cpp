@@ -510,8 +510,11 @@ struct vsg_index {
 // Everything the index owns goes back: device buffers to the pool, ordered on
 // the index's stream (the caller drained the device-search fence and the stream's
 // own work), pinned staging to the process-wide cache -- no device-wide wait.
-static void free_dev(vsg_index* h) {
+static void free_dev(vsg_index* h, PhaseClock* pc = nullptr) {
     hipStream_t st = h->stream;
+    auto mark = [&](const char* w) {
+        if (pc) pc->mark(w);
+    };
     pinned_put(h->h_plan, h->h_plan_cap, false);
     h->h_plan = nullptr;
     h->h_plan_cap = 0;
@@ -520,11 +523,14 @@ static void free_dev(vsg_index* h) {
     h->h_stg_cap = 0;
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     h->ev_pool.clear();
+    mark("free:events");
     for (SearchCtx* c : h->ctx_free) delete c;
     h->ctx_free.clear();
+    mark("free:search_contexts");
     for (Workspace* w : h->ws_free) delete w;
     h->ws_count -= std::min(h->ws_count, h->ws_free.size());
     h->ws_free.clear();
+    mark("free:workspaces");
     for (void* p : {(void*)h->d_rm, (void*)h->d_reuse, (void*)h->d_lvl_all, (void*)h->d_vecs, (void*)h->d_vecs16,
                     (void*)h->d_ktile, (void*)h->d_adj0, (void*)h->d_upper_off, (void*)h->d_upper,
                     (void*)h->d_adjd0, (void*)h->d_upperd, (void*)h->d_keys, (void*)h->d_flags,
@@ -535,6 +541,7 @@ static void free_dev(vsg_index* h) {
                     (void*)h->d_cf32, (void*)h->d_cpart_d, (void*)h->d_cpart_i, (void*)h->d_okey[0],
                     (void*)h->d_okey[1], (void*)h->d_oidx[0], (void*)h->d_oidx[1]})
         dev_free(p, st);
+    mark("free:buffers");
 }
 
 
@@ -1444,10 +1451,14 @@ void vsg_index_free(vsg_index_t* h) {
         // this index's own work only (its stream, its enqueued device searches):
         // the buffers go back to the pool in stream order, no device-wide wait
         DeviceGuard dg(h->device);
+        PhaseClock pc;  // VSG_DEBUG_TIMING=1: where a free spends its time
         h->fence.drain();
+        pc.mark("free:fence");
         hipStreamSynchronize(h->stream);
-        free_dev(h);
+        pc.mark("free:own_stream");
+        free_dev(h, &pc);
         hipStreamDestroy(h->stream);
+        pc.mark("free:stream_destroy");
     }
     delete h;
 }
@@ -1714,7 +1725,7 @@ static int add_locked(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
                 g_last_error = msg;
                 return rc;
             }
-            h->vec_gen++;  // rows are rewritten in place by the build: the f16 traversal copy goes stale
+
         }
         pc.mark("stage");
     }
@@ -1734,6 +1745,7 @@ static int add_locked(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
         // may be linked into the graph; a reused slot is a tombstone again.
         const std::string msg = g_last_error;
         unmap_keys(h, keys, n);
+        if (r) h->vec_gen++;  // staged reused rows were rewritten: the f16 copy is stale
         if (r) h->free_ring = ring_before;
         for (uint32_t s = s0; s < h->slots; ++s) h->free_ring.push_back(s);
         (void)hipMemsetAsync(h->d_flags + s0, 1, h->slots - s0, h->stream);
@@ -1744,6 +1756,18 @@ static int add_locked(vsg_index_t* h, const uint64_t* keys, const float* vecs, s
         return rc;
     }
     if (r) {  // the re-linked slots are live again
+        // their rows were rewritten in place: the f16 traversal copy gets exactly those
+        // rows re-converted (round 5 marked the whole copy stale, so the next search
+        // converted every row)
+        {
+            std::lock_guard<std::mutex> g(h->shadow_mu);
+            if (h->d_vecs16 && h->shadow_gen == h->vec_gen && h->shadow_rows > 0) {
+                const hipError_t e = launch_shadow_f16_slots(h->d_vecs, h->row_bytes, reuse_view(h, r).slots, r,
+                                                             h->shadow_rows, h->dim, h->d_vecs16, h->row_bytes16,
+                                                             h->stream);
+                if (e != hipSuccess) h->vec_gen++;  // fall back to a full re-conversion
+            }
+        }
         const hipError_t e = launch_set_flags(h->d_flags, reuse_view(h, r).slots, r, 0, h->stream);
         const hipError_t es = hipStreamSynchronize(h->stream);
         if (e != hipSuccess || es != hipSuccess)

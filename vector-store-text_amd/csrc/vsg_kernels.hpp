@@ -221,6 +221,9 @@ hipError_t launch_rerank(MetricKind mk, const RerankParams& p, hipStream_t s);
 // f32 image rows [r0, r1) -> f16 traversal copy (row_bytes16 stride, padding zeroed)
 hipError_t launch_shadow_f16(const uint8_t* vecs, size_t row_bytes, size_t r0, size_t r1, int dim,
                              uint8_t* out, size_t row_bytes16, hipStream_t s);
+// rows `slots[0..n)` (those < limit) of the f16 traversal copy, re-converted in place
+hipError_t launch_shadow_f16_slots(const uint8_t* vecs, size_t row_bytes, const uint32_t* slots, size_t n,
+                                   size_t limit, int dim, uint8_t* out, size_t row_bytes16, hipStream_t s);
 // rows [r0, r1) of row-major f32 `vecs` (row_floats % 32 == 0) -> the K-tiled layout
 // of MfmaExactParams::ktile
 hipError_t launch_ktile_rows(const float* vecs, int row_floats, size_t r0, size_t r1, float* ktile,

@@ -878,10 +878,13 @@ def host_abi_leg(c, head):
     return {"build_vectors_per_s": round(a.rows / build_s, 1), "build_seconds": round(build_s, 3),
             "build_recall_at_10": round(rb, 4),
             "qps": round(a.queries * a.steps / el, 1), "ms_per_step": round(1000.0 * el / a.steps, 3), "ef": ef,
+            "over_device_value": round(a.queries * a.steps / el / head["qps"], 3),
+            "pieces": int(os.environ.get("VSG_HOST_SEARCH_PIECES", "4")),
             "results_equal_device_search": same,
             "note": "vsg_index_add from host f32 rows (a fresh index of the same rows, PCIe included) and "
-                    "vsg_index_search with host queries and outputs over the headline index (PCIe both ways): "
-                    "the reference's add(key, &[f32]) / search(&[f32], k) call shapes, batched"}
+                    "vsg_index_search with host queries and outputs over the headline index (PCIe both ways; the "
+                    "queries uploaded in pieces, each piece's search started as it lands): the reference's "
+                    "add(key, &[f32]) / search(&[f32], k) call shapes, batched"}
 
 
 def recall_np(found, gt, k):

@@ -80,6 +80,16 @@ struct ActorBackend {
     virtual void set_error(const std::string& msg) { (void)msg; }
     virtual int search(const float* q, size_t nq, size_t k, size_t ef, uint64_t* keys, float* dist,
                        size_t* counts) = 0;
+    // the batched search of an Ann run, one pointer per query (the messages' own
+    // vectors): a backend that stages queries itself copies each straight to its
+    // staging buffer; this default gathers them and calls search()
+    virtual int search_gather(const float* const* q, size_t nq, size_t k, size_t ef, uint64_t* keys, float* dist,
+                              size_t* counts) {
+        const size_t d = dimensions();
+        std::vector<float> qs(nq * d);
+        for (size_t i = 0; i < nq; ++i) std::memcpy(&qs[i * d], q[i], d * 4);
+        return search(qs.data(), nq, k, ef, keys, dist, counts);
+    }
     virtual const char* last_error() const { return ""; }
     // stored rows including tombstones, and dropping the tombstones
     virtual size_t slots() const { return size(); }
@@ -498,7 +508,6 @@ class Actor {
 
     // ------------------------------------------------------------------ anns --
     void anns(std::vector<Msg>& b, size_t i0, size_t i1) {
-        const size_t d = be_->dimensions();
         const size_t ef0 = be_->expansion_search();
         const uint64_t t0 = steady_ns();
         {
@@ -521,7 +530,7 @@ class Actor {
                 it->second.push_back(i);
             }
         }
-        std::vector<float> qs;
+        std::vector<const float*> qs;
         std::vector<uint64_t> keys;
         std::vector<float> dist;
         std::vector<size_t> counts;
@@ -529,13 +538,13 @@ class Actor {
             const std::vector<size_t>& g = groups[e];
             size_t kmax = 0;
             for (size_t i : g) kmax = std::max(kmax, b[i].k);
-            qs.resize(g.size() * d);
-            for (size_t r = 0; r < g.size(); ++r) std::memcpy(&qs[r * d], b[g[r]].vec.data(), d * 4);
+            qs.resize(g.size());
+            for (size_t r = 0; r < g.size(); ++r) qs[r] = b[g[r]].vec.data();
             keys.resize(g.size() * kmax);
             dist.resize(g.size() * kmax);
             counts.resize(g.size());
             const uint64_t ts = steady_ns();
-            const int rc = be_->search(qs.data(), g.size(), kmax, e, keys.data(), dist.data(), counts.data());
+            const int rc = be_->search_gather(qs.data(), g.size(), kmax, e, keys.data(), dist.data(), counts.data());
             const uint64_t tn = steady_ns();
             {
                 std::lock_guard<std::mutex> lk(cm_);

@@ -10,6 +10,8 @@
 
 namespace vsg {
 void set_last_error(const std::string& msg);  // vsg_index.cpp
+int index_search_gather(vsg_index_t* h, const float* const* q, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
+                        float* out_distances, size_t* out_counts);
 }
 
 namespace {
@@ -39,6 +41,10 @@ struct IndexBackend final : vsg::ActorBackend {
     int search(const float* q, size_t nq, size_t k, size_t e, uint64_t* keys, float* dist,
                size_t* counts) override {
         return vsg_index_search(h, q, nq, k, e, keys, dist, counts);
+    }
+    int search_gather(const float* const* q, size_t nq, size_t k, size_t e, uint64_t* keys, float* dist,
+                      size_t* counts) override {
+        return vsg::index_search_gather(h, q, nq, k, e, keys, dist, counts);
     }
     size_t slots() const override {
         size_t s = 0;

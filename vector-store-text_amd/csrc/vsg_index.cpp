@@ -2572,9 +2572,12 @@ static int search_host_pieces(vsg_index* h, SearchCtx* c, const float* queries, 
     return rc;
 }
 
+// qptrs (optional, instead of `queries`): one pointer per query -- the actor's
+// messages -- gathered straight into the pinned staging (one host copy, not two).
 static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
-                       float* out_dist, size_t* out_counts, bool exact) {
-    if (!h || (!queries && nq) || (!out_keys && nq) || (!out_dist && nq)) return fail(VSG_EINVAL, "null argument");
+                       float* out_dist, size_t* out_counts, bool exact, const float* const* qptrs = nullptr) {
+    if (!h || (!queries && !qptrs && nq) || (!out_keys && nq) || (!out_dist && nq))
+        return fail(VSG_EINVAL, "null argument");
     if (k == 0) return fail(VSG_EINVAL, "k must be >= 1 (Limit is NonZeroUsize)");
     if (nq == 0) return VSG_OK;
     const auto wall0 = std::chrono::steady_clock::now();
@@ -2587,7 +2590,7 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
     static const size_t max_pieces = std::min<size_t>(
         SearchCtx::PIECES, std::max<size_t>(1, (size_t)env_double("VSG_HOST_SEARCH_PIECES", SearchCtx::PIECES)));
     // pieces only where the upload is worth hiding (>= 16 MiB of queries, >= 1,024 per piece)
-    const size_t P = !exact && nq * h->dim * 4 >= ((size_t)16 << 20)
+    const size_t P = !exact && !qptrs && nq * h->dim * 4 >= ((size_t)16 << 20)
                          ? std::min(max_pieces, std::max<size_t>(1, nq / 1024)) : 1;
     // pinned: queries, then (pieces) a separate results area -- a piece's results come
     // back while later pieces' queries are still being copied in
@@ -2621,7 +2624,15 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
         float* dd = reinterpret_cast<float*>(c->dev + qb + kb);
         uint32_t* dc = reinterpret_cast<uint32_t*>(c->dev + qb + kb + db);
         mark(0);
-        if (h2d_staged(dq, c->pin, queries, nq * h->dim * 4, c->s) != hipSuccess) {
+        hipError_t eu = hipSuccess;
+        if (qptrs) {
+            const size_t row = (size_t)h->dim * 4;
+            for (size_t i = 0; i < nq; ++i) std::memcpy(c->pin + i * row, qptrs[i], row);
+            eu = copy_chunked(dq, c->pin, nq * row, hipMemcpyHostToDevice, c->s);
+        } else {
+            eu = h2d_staged(dq, c->pin, queries, nq * h->dim * 4, c->s);
+        }
+        if (eu != hipSuccess) {
             rc = fail(VSG_EDEVICE, "H2D queries");
         } else {
             mark(1);
@@ -2655,6 +2666,14 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
     h->hs_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - wall0).count();
     return rc;
 }
+
+namespace vsg {
+// the actor's batched search (vsg_actor.cpp): queries gathered from its messages
+int index_search_gather(vsg_index_t* h, const float* const* q, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
+                        float* out_distances, size_t* out_counts) {
+    return search_host(h, nullptr, nq, k, ef, out_keys, out_distances, out_counts, false, q);
+}
+}  // namespace vsg
 
 int vsg_index_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
                      float* out_distances, size_t* out_counts) {

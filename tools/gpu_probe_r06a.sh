@@ -9,10 +9,13 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 out=gpurun_out/r06_phases.jsonl
-for v in prof base; do
+for v in prof base ce; do
   lib=vector-store-text_amd/lib/libvsg.so
   ph=""
   [ "$v" = prof ] && lib=vector-store-text_amd/lib_prof/libvsg.so && ph="--phases"
+  # ce: the compaction stops at the first prefix range that fits (VSG_COMPACT_EARLY)
+  [ "$v" = ce ] && lib=vector-store-text_amd/lib_ce/libvsg.so
+  [ -f "$lib" ] || continue
   for nq in 512 10000; do
     VSG_LIB_PATH=$lib timeout -k 10 240 python3 -u tools/gpu_probe.py search --queries $nq --gt-queries $nq \
       --efs 36 --steps 5 $ph \

@@ -48,6 +48,49 @@ static int fail(int code, const std::string& msg) {
 namespace vsg {
 // shared by the other C-ABI translation units (vsg_actor.cpp)
 void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+// Non-blocking streams, recycled process-wide per device.  On the MI355X box a
+// hipStreamCreate took 7.8 ms and a hipStreamDestroy 2.3 ms while another stream
+// was busy (tools/free_probe, profiles/r06_free_probe.json), so an index free
+// -- its own stream and up to 4 per pooled search context -- cost ~10 ms and
+// more.  A stream comes back idle (its owner synchronised it) and is handed to
+// the next index or context on the same device.
+struct StreamCache {
+    std::mutex mu;
+    std::vector<std::pair<int, hipStream_t>> idle;
+};
+static StreamCache& stream_cache() {
+    static StreamCache* c = new StreamCache;  // never destroyed (streams outlive statics)
+    return *c;
+}
+hipError_t stream_get(hipStream_t* s) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    {
+        StreamCache& c = stream_cache();
+        std::lock_guard<std::mutex> lk(c.mu);
+        for (size_t i = c.idle.size(); i-- > 0;)
+            if (c.idle[i].first == dev) {
+                *s = c.idle[i].second;
+                c.idle.erase(c.idle.begin() + (long)i);
+                return hipSuccess;
+            }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+// s must be idle (synchronised by the caller); nullptr: nothing
+void stream_put(hipStream_t s) {
+    if (!s) return;
+    hipDevice_t dev = 0;
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) {
+        (void)hipStreamDestroy(s);
+        return;
+    }
+    StreamCache& c = stream_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.idle.push_back({(int)dev, s});
+}
 }
 
 #define HIP_TRY(expr)                                                                        \
@@ -249,6 +292,14 @@ struct PhaseClock {
 
 }  // namespace
 
+// the same pool, pinned cache and stream cache for the sharded index (vsg_sharded.cpp)
+namespace vsg {
+hipError_t pool_malloc(void** p, size_t bytes, hipStream_t s) { return pool_alloc(p, bytes, s); }
+void pool_free(void* p, hipStream_t s) { dev_free(p, s); }
+hipError_t pinned_take(uint8_t** p, size_t* cap, size_t want, bool coherent) { return pinned_get(p, cap, want, coherent); }
+void pinned_return(uint8_t* p, size_t cap, bool coherent) { pinned_put(p, cap, coherent); }
+}  // namespace vsg
+
 // Reusable context of one host-buffer search call: a stream, pinned staging
 // and device buffers that only grow.  Pooled per index so concurrent callers
 // (and the actor's worker) pay no stream creation / pageable copies per call.
@@ -272,9 +323,11 @@ struct SearchCtx {
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : pev)
             if (e) (void)hipEventDestroy(e);
-        for (int i = 1; i < PIECES; ++i)
-            if (ps[i]) (void)hipStreamDestroy(ps[i]);
-        if (s) (void)hipStreamDestroy(s);
+        for (int i = 1; i < PIECES; ++i) {
+            if (ps[i]) (void)hipStreamSynchronize(ps[i]);
+            stream_put(ps[i]);
+        }
+        stream_put(s);
     }
 };
 
@@ -1430,13 +1483,15 @@ int vsg_index_new(const vsg_index_options_t* o, vsg_index_t** out) {
         return fail(VSG_EINVAL, "device ordinal out of range");
     }
     DeviceGuard dg(h->device);
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (stream_get(&h->stream) != hipSuccess) {
         delete h;
         return fail(VSG_EDEVICE, "hipStreamCreate failed");
     }
     if (dev_alloc(&h->d_stats, VSG_NSTATS, h->stream) != hipSuccess ||
         hipMemsetAsync(h->d_stats, 0, VSG_NSTATS * sizeof(unsigned long long), h->stream) != hipSuccess ||
         hipStreamSynchronize(h->stream) != hipSuccess) {
+        dev_free(h->d_stats, h->stream);
+        if (hipStreamSynchronize(h->stream) == hipSuccess) stream_put(h->stream);
         delete h;
         return fail(VSG_ENOMEM, "stats allocation failed");
     }
@@ -1457,8 +1512,8 @@ void vsg_index_free(vsg_index_t* h) {
         hipStreamSynchronize(h->stream);
         pc.mark("free:own_stream");
         free_dev(h, &pc);
-        hipStreamDestroy(h->stream);
-        pc.mark("free:stream_destroy");
+        stream_put(h->stream);  // idle (synchronised above): recycled, not destroyed
+        pc.mark("free:stream_put");
     }
     delete h;
 }
@@ -2418,7 +2473,7 @@ static SearchCtx* ctx_acquire(vsg_index* h) {
         }
     }
     SearchCtx* c = new SearchCtx;
-    if (hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
+    if (stream_get(&c->s) != hipSuccess) {
         delete c;
         return nullptr;
     }
@@ -2544,7 +2599,7 @@ static int search_host_pieces(vsg_index* h, SearchCtx* c, const float* queries, 
     for (size_t i = 0; i < P; ++i) {
         marks[i] = (i + 1) * nq / P * row;
         if (!c->pev[i]) HIP_TRY(hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming));
-        if (i && !c->ps[i]) HIP_TRY(hipStreamCreateWithFlags(&c->ps[i], hipStreamNonBlocking));
+        if (i && !c->ps[i]) HIP_TRY(stream_get(&c->ps[i]));
     }
     c->ps[0] = c->s;
     if (h2d_staged(dq, c->pin, queries, nq * row, c->s, marks, P, c->pev) != hipSuccess)
@@ -2667,13 +2722,16 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
     return rc;
 }
 
+}  // extern "C"
 namespace vsg {
 // the actor's batched search (vsg_actor.cpp): queries gathered from its messages
+// (C++ linkage: outside the ABI block)
 int index_search_gather(vsg_index_t* h, const float* const* q, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
                         float* out_distances, size_t* out_counts) {
     return search_host(h, nullptr, nq, k, ef, out_keys, out_distances, out_counts, false, q);
 }
 }  // namespace vsg
+extern "C" {
 
 int vsg_index_search(vsg_index_t* h, const float* queries, size_t nq, size_t k, size_t ef, uint64_t* out_keys,
                      float* out_distances, size_t* out_counts) {

@@ -33,6 +33,14 @@
 namespace vsg {
 void set_last_error(const std::string& msg);  // vsg_index.cpp
 size_t index_first_live(const vsg_index_t* h, const uint64_t* keys, size_t n);
+// vsg_index.cpp: the per-device memory pool (stream-ordered frees, no device-wide
+// wait), the process-wide pinned and stream caches
+hipError_t pool_malloc(void** p, size_t bytes, hipStream_t s);
+void pool_free(void* p, hipStream_t s);
+hipError_t pinned_take(uint8_t** p, size_t* cap, size_t want, bool coherent);
+void pinned_return(uint8_t* p, size_t cap, bool coherent);
+hipError_t stream_get(hipStream_t* s);
+void stream_put(hipStream_t s);
 }  // namespace vsg
 
 namespace {
@@ -87,14 +95,16 @@ void per_shard(size_t n, F&& f) {
     for (auto& t : th) t.join();
 }
 
+// grow a device buffer on stream s (the old block returns to the pool after s's
+// earlier work; callers have waited for other streams' readers)
 template <typename X>
-hipError_t grow(X** p, size_t& cap, size_t bytes) {
+hipError_t grow(X** p, size_t& cap, size_t bytes, hipStream_t s) {
     if (bytes <= cap) return hipSuccess;
     const size_t want = std::max(bytes, cap * 2);
-    if (*p) (void)hipFree(*p);
+    vsg::pool_free(*p, s);
     *p = nullptr;
     cap = 0;
-    const hipError_t e = hipMalloc((void**)p, want);
+    const hipError_t e = vsg::pool_malloc((void**)p, want, s);
     if (e == hipSuccess) cap = want;
     return e;
 }
@@ -143,29 +153,35 @@ struct vsg_sharded {
 static void ctx_destroy(vsg_sharded* h, ShardCtx* c) {
     for (size_t g = 0; g < c->s.size(); ++g) {
         DevGuard dg(h->dev[g]);
-        if (c->s[g]) {
-            (void)hipStreamSynchronize(c->s[g]);
-            (void)hipStreamDestroy(c->s[g]);
-        }
+        if (c->s[g]) (void)hipStreamSynchronize(c->s[g]);
         if (c->ev[g]) (void)hipEventDestroy(c->ev[g]);
-        if (c->out[g]) (void)hipFree(c->out[g]);
+    }
+    DevGuard dga(h->ans);
+    if (c->sa) (void)hipStreamSynchronize(c->sa);
+    if (c->pending) (void)hipEventSynchronize(c->done);
+    // every stream of the context is idle: buffers back to their device's pool
+    // (ordered on an idle stream of that device), streams back to the cache
+    for (size_t g = 0; g < c->s.size(); ++g) {
+        DevGuard dg(h->dev[g]);
+        vsg::pool_free(c->out[g], c->s[g]);
     }
     for (size_t d = 0; d < c->q.size(); ++d) {
         DevGuard dg(h->devs[d]);
-        if (c->q[d]) (void)hipFree(c->q[d]);
+        vsg::pool_free(c->q[d], c->s[h->first_on[d]]);
         if (c->q_ev[d]) (void)hipEventDestroy(c->q_ev[d]);
     }
-    DevGuard dg(h->ans);
-    if (c->sa) {
-        (void)hipStreamSynchronize(c->sa);
-        (void)hipStreamDestroy(c->sa);
+    vsg::pool_free(c->gather, c->sa);
+    vsg::pool_free(c->res, c->sa);
+    for (size_t g = 0; g < c->s.size(); ++g) {
+        DevGuard dg(h->dev[g]);
+        if (c->s[g]) (void)hipStreamSynchronize(c->s[g]);
+        vsg::stream_put(c->s[g]);
     }
-    if (c->pending) (void)hipEventSynchronize(c->done);
+    if (c->sa) (void)hipStreamSynchronize(c->sa);
+    vsg::stream_put(c->sa);
     if (c->start) (void)hipEventDestroy(c->start);
     if (c->done) (void)hipEventDestroy(c->done);
-    if (c->gather) (void)hipFree(c->gather);
-    if (c->res) (void)hipFree(c->res);
-    if (c->pin) (void)hipHostFree(c->pin);
+    vsg::pinned_return(c->pin, c->pin_cap, true);
     delete c;
 }
 
@@ -189,7 +205,7 @@ static int ctx_acquire(vsg_sharded* h, ShardCtx** out) {
     hipError_t e = hipSuccess;
     for (uint32_t g = 0; g < h->n && e == hipSuccess; ++g) {
         DevGuard dg(h->dev[g]);
-        e = hipStreamCreateWithFlags(&c->s[g], hipStreamNonBlocking);
+        e = vsg::stream_get(&c->s[g]);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev[g], hipEventDisableTiming);
     }
     for (size_t d = 0; d < h->devs.size() && e == hipSuccess; ++d) {
@@ -198,7 +214,7 @@ static int ctx_acquire(vsg_sharded* h, ShardCtx** out) {
     }
     if (e == hipSuccess) {
         DevGuard dg(h->ans);
-        e = hipStreamCreateWithFlags(&c->sa, hipStreamNonBlocking);
+        e = vsg::stream_get(&c->sa);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->start, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
     }
@@ -232,7 +248,7 @@ static int search_enqueue(vsg_sharded* h, ShardCtx* c, const float* q, size_t nq
     }
     {
         DevGuard dg(h->ans);
-        SH_TRY(grow(&c->gather, c->gather_cap, n * (kb + db)));
+        SH_TRY(grow(&c->gather, c->gather_cap, n * (kb + db), sa));
         SH_TRY(hipEventRecord(c->start, sa));
     }
     uint8_t* gk = c->gather;
@@ -243,7 +259,7 @@ static int search_enqueue(vsg_sharded* h, ShardCtx* c, const float* q, size_t nq
         if (dv == h->ans) continue;
         const int g0 = h->first_on[d];
         DevGuard dg(dv);
-        SH_TRY(grow(&c->q[d], c->q_cap[d], nq * dim * 4));
+        SH_TRY(grow(&c->q[d], c->q_cap[d], nq * dim * 4, c->s[g0]));
         if (c->pending) SH_TRY(hipStreamWaitEvent(c->s[g0], c->done, 0));
         SH_TRY(hipStreamWaitEvent(c->s[g0], c->start, 0));
         SH_TRY(hipMemcpyPeerAsync(c->q[d], dv, q, h->ans, nq * dim * 4, c->s[g0]));
@@ -266,7 +282,7 @@ static int search_enqueue(vsg_sharded* h, ShardCtx* c, const float* q, size_t nq
                 SH_TRY(hipStreamWaitEvent(st, c->q_ev[d], 0));
             }
             qg = reinterpret_cast<const float*>(c->q[d]);
-            SH_TRY(grow(&c->out[g], c->out_cap[g], kb + db));
+            SH_TRY(grow(&c->out[g], c->out_cap[g], kb + db, st));
             K = reinterpret_cast<uint64_t*>(c->out[g]);
             D = reinterpret_cast<float*>(c->out[g] + kb);
         }
@@ -313,13 +329,12 @@ static int search_host(vsg_sharded* h, const float* queries, size_t nq, size_t k
     hipError_t e = hipSuccess;
     {
         DevGuard dg(h->ans);
-        e = grow(&c->res, c->res_cap, qb + kb + db);
+        e = grow(&c->res, c->res_cap, qb + kb + db, c->sa);
         if (e == hipSuccess && std::max(qb, kb + db) > c->pin_cap) {
-            if (c->pin) (void)hipHostFree(c->pin);
+            vsg::pinned_return(c->pin, c->pin_cap, true);
             c->pin = nullptr;
             c->pin_cap = 0;
-            e = hipHostMalloc((void**)&c->pin, std::max(qb, kb + db), hipHostMallocCoherent);
-            if (e == hipSuccess) c->pin_cap = std::max(qb, kb + db);
+            e = vsg::pinned_take(&c->pin, &c->pin_cap, std::max(qb, kb + db), true);
         }
         if (e == hipSuccess) {
             std::memcpy(c->pin, queries, nq * h->opt.dimensions * 4);
@@ -507,9 +522,10 @@ int vsg_sharded_add(vsg_sharded_t* h, const uint64_t* keys, const float* vectors
         float* pin = nullptr;
         hipStream_t st = nullptr;
         const size_t piece = std::min<size_t>(ng, std::max<size_t>(1, ((size_t)16 << 20) / (dim * 4)));
-        hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipMalloc((void**)&dv, ng * dim * 4);
-        if (e == hipSuccess) e = hipHostMalloc((void**)&pin, piece * dim * 4, hipHostMallocDefault);
+        size_t pin_cap = 0;
+        hipError_t e = vsg::stream_get(&st);
+        if (e == hipSuccess) e = vsg::pool_malloc((void**)&dv, ng * dim * 4, st);
+        if (e == hipSuccess) e = vsg::pinned_take(reinterpret_cast<uint8_t**>(&pin), &pin_cap, piece * dim * 4, false);
         for (size_t off = 0; off < ng && e == hipSuccess; off += piece) {
             const size_t c = std::min(piece, ng - off);
             for (size_t j = 0; j < c; ++j)
@@ -525,9 +541,12 @@ int vsg_sharded_add(vsg_sharded_t* h, const uint64_t* keys, const float* vectors
             if (rc[g]) msg[g] = vsg_last_error();  // thread-local: read on this thread
         }
         if (st) (void)hipStreamSynchronize(st);
-        if (pin) (void)hipHostFree(pin);
-        if (dv) (void)hipFree(dv);
-        if (st) (void)hipStreamDestroy(st);
+        vsg::pinned_return(reinterpret_cast<uint8_t*>(pin), pin_cap, false);
+        if (st) {
+            vsg::pool_free(dv, st);
+            (void)hipStreamSynchronize(st);
+            vsg::stream_put(st);
+        }
     });
     size_t bad = h->n;
     for (size_t g = 0; g < h->n; ++g)

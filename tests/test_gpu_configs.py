@@ -176,6 +176,7 @@ def test_c4_100m128_f16_eight_row_shards_merged():
             ork.append(sk)
             ord_.append(sd)
             parts.append(idx)
+            print(f"C4 shard {s}: built, oracle exact top-{k} done", flush=True)  # progress (long test)
     finally:
         O.set_fast_metric(False)
     assert sum(p.size() for p in parts) == n

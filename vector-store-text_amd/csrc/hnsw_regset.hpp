@@ -289,6 +289,15 @@ __device__ __forceinline__ void admit(RegSet<R>& B, bool mine, uint64_t ck, bool
 // slower: the runner-up is rarely still next (profiles/r01_search_phases.jsonl).
 // Prefetching only the runner-up's adjacency row: C4 shard search -8 %, C2
 // search +2 %, C2 build -5 % (profiles/r02_search_probes.jsonl) -- not kept.
+// Round 6 loaded the row of the exact next expansion (the smallest of B's
+// unexpanded keys and this batch's candidates below tkey, known before the
+// admit) under the admit and compaction: bit-exact, but no faster at 512 or 10k
+// queries (C2 0.523 -> 0.526 ms, 2.954 -> 2.978 ms; C4 shard ef 192 3.08 -> 3.27 ms
+// with 12 more VGPRs, profiles/r06_prefetch_ab.jsonl).  The SQ counters of the C4
+// shard search say why: waves issue 34 % of their cycles, stall on issue 21 %,
+// wait on memory 45 %, and the SIMDs' issue slots are nearly all taken
+// (profiles/r06_c4_sq.json) -- latency is hidden by the other resident waves, so a
+// shorter chain per wave does not shorten the launch.  Not kept.
 // self: the node an insert (re)links, never admitted (VSG_EMPTY in searches).
 template <int G, int VM, int U, typename T, int MET, int R>
 __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>& q, int l, uint32_t ep, float dep, int ef, WaveLds& w,
@@ -334,22 +343,10 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
     auto row_of = [&](uint32_t n) {
         return l == 0 ? adj0 + (size_t)n * m0r : upper + ((size_t)upper_off[n] + (size_t)(l - 1)) * mr;
     };
-    // The next expansion is known as soon as this one's distances are: the
-    // smallest of B's unexpanded keys and the candidates below tkey (the admit
-    // only adds those, a compaction only drops keys above its cut).  Its
-    // adjacency row is loaded then, so the load runs under the admit and the
-    // compaction instead of after them.  If a compaction dropped it (pred > the
-    // new tkey), every unexpanded key was above the cut too and the beam ends,
-    // as min_unexpanded would say.  Rows of <= 64 entries (one piece) and exact
-    // visited tables only; otherwise the selection below.
-    const bool predict = m <= 64;
-    bool have_pred = false;
-    uint64_t pred = VSG_KEY_EMPTY;
-    uint32_t nb_pred = VSG_EMPTY;
     for (;;) {
         const uint64_t t0 = VSG_CLK();
         [[maybe_unused]] uint64_t c0c = VSG_CYC();
-        const uint64_t a = have_pred ? (pred <= B.tkey ? pred : VSG_KEY_EMPTY) : B.min_unexpanded();
+        const uint64_t a = B.min_unexpanded();
         if (a == VSG_KEY_EMPTY) break;
         if (B.size > ef && B.count_below(a) >= ef) break;
         B.mark_expanded(a);
@@ -368,7 +365,7 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
         // pieces are admitted one after another, which leaves the same set as one
         // batch (B only ever keeps the best ef of everything evaluated)
         for (int c0 = 0; c0 < m; c0 += 64) {
-            const uint32_t nb = have_pred ? nb_pred : c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
+            const uint32_t nb = c0 + lane < m ? row[c0 + lane] : VSG_EMPTY;
             const bool full = __ballot(nb != VSG_EMPTY) == ~0ull;
 #ifdef VSG_SEARCH_PROFILE
             {
@@ -393,7 +390,6 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
                 c0c = c;
             }
 #endif
-            uint64_t ck = VSG_KEY_EMPTY;
             if (cnt) {
 #ifdef VSG_SEARCH_PROFILE
                 rows_dist<G, VM, U, T, MET>(g.vecs, g.row_bytes, g.nchunks, w.todo, cnt, q, w.tdist, &pf.rows);
@@ -402,25 +398,7 @@ __device__ __forceinline__ void beam_reg(const GraphDev& g, const QReg<G, VM, T>
 #endif
                 wave_sync();
                 ndist += (uint64_t)cnt;
-                if (lane < cnt) ck = cand_key(w.tdist[lane], w.todo[lane]);
-            }
-            have_pred = predict && !lossy;
-            if (have_pred) {
-                uint64_t b = ck < B.tkey ? ck : VSG_KEY_EMPTY;
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-                    if (!((B.expm >> r) & 1u) && B.k[r] < b) b = B.k[r];
-                pred = wave_min64(b);
-                // a relaxed wave-scope atomic load is a plain global_load_dword, but the
-                // compiler does not merge it with the row load of the next iteration
-                // (which sank a plain load back to its use, undoing the early issue)
-                nb_pred = VSG_EMPTY;
-                if (pred != VSG_KEY_EMPTY && lane < m)
-                    nb_pred = __hip_atomic_load(
-                        (__attribute__((address_space(1))) const uint32_t*)(row_of((uint32_t)pred & VSG_ID_MASK) + lane),
-                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            }
-            if (cnt) {
+                const uint64_t ck = lane < cnt ? cand_key(w.tdist[lane], w.todo[lane]) : VSG_KEY_EMPTY;
                 const uint64_t t2 = VSG_CLK();
                 pf.dist += t2 - t1;
 #ifdef VSG_SEARCH_PROFILE

@@ -154,14 +154,8 @@ __device__ __forceinline__ void search_reg_one(const SearchParams& p, int qi, ui
 // the same constant.
 template <int G, int VM> constexpr bool persist_shape() { return G * VM * 16 >= 1024; }
 
-// Occupancy floor of the short-row instances (rows <= 256 B, <= 4 register rows: the C4
-// shard's 128-d f16): 5 waves per SIMD.  The early next-expansion load (beam_reg) put
-// them at 99 VGPRs (4 waves) when left to the allocator.
-template <int G, int VM, int R> constexpr int search_min_waves() { return G * VM * 16 <= 256 && R <= 4 ? 5 : 1; }
-
 template <int G, int VM, int U, typename T, int MET, int R>
-__global__ __launch_bounds__(64) VSG_SEARCH_ATTR
-__attribute__((amdgpu_waves_per_eu(search_min_waves<G, VM, R>()))) void hnsw_search_reg_kernel(SearchParams p) {
+__global__ __launch_bounds__(64) VSG_SEARCH_ATTR void hnsw_search_reg_kernel(SearchParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if constexpr (persist_shape<G, VM>()) {
         if (p.qnext) {

@@ -238,7 +238,10 @@ __device__ __forceinline__ void mask_tail(uint4 (&raw)[VM], int nchunks, int sl)
 // distance (l2sq, or 1 - dot).  All U x VM chunk loads of a pass are issued
 // before any arithmetic and kept as raw 16-B words (4 VGPRs each; f16 rows are
 // widened to f32 only when consumed), so the loads in flight cost half the
-// registers for f16 rows.
+// registers for f16 rows.  A pass whose rows all lie past `count` is skipped
+// (the last round of a call is mostly short: ~19 fresh rows of a C4 expansion
+// filled 2.4 of the 4 passes of 8 rows, and the other 1.6 used to load and
+// reduce copies of the last row -- 40 % of the distance VALU; round 6).
 // Search-profile clock (shader cycles, s_memtime; the make prof build only).
 #ifdef VSG_SEARCH_PROFILE
 #define VSG_CYC() __builtin_amdgcn_s_memtime()
@@ -251,6 +254,13 @@ struct RowsProf {
     uint64_t wait = 0, valu = 0;
     uint32_t passes = 0;
 };
+
+// Loads of a pass past `count` are skipped only for rows of <= 512 B: with a
+// conditional load the compiler can no longer count the loads in flight, so the
+// first pass's arithmetic waits for every pass's loads (vmcnt(0)); long rows lose
+// that overlap (C2 512 queries 0.52 -> 0.547 ms), short rows gain more from the
+// skipped loads than they lose (C4 shard ef 192 3.10 -> 2.87 ms; round 6).
+template <int G, int VM> constexpr bool kSkipLoads() { return G * VM * 16 <= 512; }
 
 template <int G, int VM, int U, typename T, int MET>
 __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size_t row_bytes,
@@ -266,6 +276,7 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
         uint4 raw[U][VM];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            if (kSkipLoads<G, VM>() && base + u * R >= count) break;  // wave-uniform: no row listed
             const int r = base + u * R + sub;
             const int rr = r < count ? r : count - 1;
             const uint8_t* row = vecs + (size_t)ids[rr] * row_bytes;
@@ -288,6 +299,7 @@ __device__ __forceinline__ void rows_dist(const uint8_t* __restrict__ vecs, size
 #endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            if (base + u * R >= count) break;
             float acc = 0.f;
             mask_tail<G, VM, MET>(raw[u], nchunks, sl);
 #pragma unroll
@@ -323,6 +335,7 @@ __device__ __forceinline__ void rows_dist2(const uint8_t* __restrict__ vecs, siz
         uint4 raw[U][VM];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            if (kSkipLoads<G, VM>() && base + u * R >= count) break;  // wave-uniform: no row listed
             const int r = base + u * R + sub;
             const int rr = r < count ? r : count - 1;
             const uint8_t* row = vecs + (size_t)ids[rr] * row_bytes;
@@ -334,6 +347,7 @@ __device__ __forceinline__ void rows_dist2(const uint8_t* __restrict__ vecs, siz
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            if (base + u * R >= count) break;
             float a0 = 0.f, a1 = 0.f;
             mask_tail<G, VM, MET>(raw[u], nchunks, sl);
 #pragma unroll
@@ -376,6 +390,7 @@ __device__ __forceinline__ uint32_t rows_test(const uint8_t* __restrict__ vecs, 
         uint4 raw[U][VM];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            if (kSkipLoads<G, VM>() && base + u * R >= count) break;  // wave-uniform: no row listed
             const int r = base + u * R + sub;
             const int rr = r < count ? r : count - 1;
             const uint8_t* row = vecs + (size_t)ids[rr] * row_bytes;
@@ -387,6 +402,7 @@ __device__ __forceinline__ uint32_t rows_test(const uint8_t* __restrict__ vecs, 
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            if (base + u * R >= count) break;
             float a[NQ];
 #pragma unroll
             for (int j = 0; j < NQ; ++j) a[j] = 0.f;

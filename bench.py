@@ -879,11 +879,11 @@ def host_abi_leg(c, head):
             "build_recall_at_10": round(rb, 4),
             "qps": round(a.queries * a.steps / el, 1), "ms_per_step": round(1000.0 * el / a.steps, 3), "ef": ef,
             "over_device_value": round(a.queries * a.steps / el / head["qps"], 3),
-            "pieces": int(os.environ.get("VSG_HOST_SEARCH_PIECES", "4")),
+            "pieces": int(os.environ.get("VSG_HOST_SEARCH_PIECES", "1")),
             "results_equal_device_search": same,
             "note": "vsg_index_add from host f32 rows (a fresh index of the same rows, PCIe included) and "
-                    "vsg_index_search with host queries and outputs over the headline index (PCIe both ways; the "
-                    "queries uploaded in pieces, each piece's search started as it lands): the reference's "
+                    "vsg_index_search with host queries and outputs over the headline index (PCIe both ways; "
+                    "queries staged through pinned memory by 8 host threads, 4-MiB DMA pieces): the reference's "
                     "add(key, &[f32]) / search(&[f32], k) call shapes, batched"}
 
 

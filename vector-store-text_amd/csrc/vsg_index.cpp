@@ -311,7 +311,7 @@ struct SearchCtx {
     size_t dev_cap = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // VSG_PROFILE_HOST_SEARCH: H2D | kernels | D2H
     // pipelined large calls (search_host): piece i's queries are in (pev[i], recorded
-    // on s by the upload) and its search + result copy run on ps[i] (ps[0] = s)
+    // on s by the upload) and its search + result copy run on ps[i] (streams of their own; s carries only the uploads)
     static constexpr int PIECES = 4;
     hipStream_t ps[PIECES] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t pev[PIECES] = {nullptr, nullptr, nullptr, nullptr};
@@ -323,7 +323,7 @@ struct SearchCtx {
             if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : pev)
             if (e) (void)hipEventDestroy(e);
-        for (int i = 1; i < PIECES; ++i) {
+        for (int i = 0; i < PIECES; ++i) {
             if (ps[i]) (void)hipStreamSynchronize(ps[i]);
             stream_put(ps[i]);
         }
@@ -2599,9 +2599,8 @@ static int search_host_pieces(vsg_index* h, SearchCtx* c, const float* queries, 
     for (size_t i = 0; i < P; ++i) {
         marks[i] = (i + 1) * nq / P * row;
         if (!c->pev[i]) HIP_TRY(hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming));
-        if (i && !c->ps[i]) HIP_TRY(stream_get(&c->ps[i]));
+        if (!c->ps[i]) HIP_TRY(stream_get(&c->ps[i]));
     }
-    c->ps[0] = c->s;
     if (h2d_staged(dq, c->pin, queries, nq * row, c->s, marks, P, c->pev) != hipSuccess)
         return fail(VSG_EDEVICE, "H2D queries");
     uint64_t* rk = reinterpret_cast<uint64_t*>(pres);
@@ -2610,8 +2609,8 @@ static int search_host_pieces(vsg_index* h, SearchCtx* c, const float* queries, 
     int rc = VSG_OK;
     for (size_t i = 0; i < P && rc == VSG_OK; ++i) {
         const size_t q0 = i * nq / P, q1 = (i + 1) * nq / P;
-        hipStream_t si = c->ps[i];
-        if (i) HIP_TRY(hipStreamWaitEvent(si, c->pev[i], 0));
+        hipStream_t si = c->ps[i];  // every piece on its own stream: c->s carries only the uploads
+        HIP_TRY(hipStreamWaitEvent(si, c->pev[i], 0));
         rc = search_device_locked(h, reinterpret_cast<const float*>(dq + q0 * row), q1 - q0, k, ef, dk + q0 * k,
                                   dd + q0 * k, dc + q0, si, exact);
         if (rc) break;
@@ -2642,8 +2641,13 @@ static int search_host(vsg_index_t* h, const float* queries, size_t nq, size_t k
     if (!c) return fail(VSG_EDEVICE, "hipStreamCreate failed");
     const size_t qb = align256(nq * h->dim * 4), kb = align256(nq * k * 8), db = align256(nq * k * 4),
                  cb = align256(nq * 4);
+    // VSG_HOST_SEARCH_PIECES (default 1): pieces each searched on its own stream as its
+    // queries land.  Measured at C2, 10k queries, ef 36 (profiles/r06_host_pieces.jsonl):
+    // 1 / 2 / 4 pieces 3.87 / 4.02 / 4.08 ms per call against 2.92 ms device-resident --
+    // a 2,500-query launch carries the same tail as a 10k one, so splitting the search
+    // costs more than the overlapped upload saves.
     static const size_t max_pieces = std::min<size_t>(
-        SearchCtx::PIECES, std::max<size_t>(1, (size_t)env_double("VSG_HOST_SEARCH_PIECES", SearchCtx::PIECES)));
+        SearchCtx::PIECES, std::max<size_t>(1, (size_t)env_double("VSG_HOST_SEARCH_PIECES", 1)));
     // pieces only where the upload is worth hiding (>= 16 MiB of queries, >= 1,024 per piece)
     const size_t P = !exact && !qptrs && nq * h->dim * 4 >= ((size_t)16 << 20)
                          ? std::min(max_pieces, std::max<size_t>(1, nq / 1024)) : 1;

@@ -25,6 +25,12 @@
  * not while the graph is built, so a search issued during a long batched build
  * answers at once from the last completed state (plus any rows of the build in
  * flight it reaches through new links -- a prefix of the writes).
+ *
+ * Memory: every device buffer comes from one stream-ordered memory pool per
+ * device and is returned with hipFreeAsync on its owner's stream; streams and
+ * pinned staging are recycled process-wide.  No call waits for another index's
+ * device work: freeing or growing an index beside another index's build or
+ * search returns in milliseconds (tests/test_gpu_concurrency.py).
  */
 #ifndef VSG_H
 #define VSG_H

@@ -822,11 +822,13 @@ def actor_serving_leg(a, ef, clients_list=(512, 2048), total=51200):
     if not os.path.exists(exe):
         return {"error": "tools/actor_load not built (__graft_entry__.build)"}
     out = {"note": "closed-loop clients of single-query vsg_actor_ann_cb (completion = the reference's "
-                   "oneshot), one actor worker; index rebuilt in the child with the headline rows/seed",
+                   "oneshot), one read worker beside the write FIFO (concurrent_reads = 1, the Rust drop-in's "
+                   "setting, rust/src/index/gpu.rs); index rebuilt in the child with the headline rows/seed",
+           "read_workers": 1,
            "ef": ef}
     for cl in clients_list:
         cmd = [exe, str(a.rows), str(a.dim), str({"l2sq": 0, "ip": 1, "cos": 2}[a.metric]), str(cl),
-               str(max(1, total // cl)), str(a.k), str(ef), "0", "0", "1", str(0x5EED)]
+               str(max(1, total // cl)), str(a.k), str(ef), "0", "1", "1", str(0x5EED)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]

@@ -3177,11 +3177,12 @@ struct FileCloser {
     }
 };
 
+// staging of save / load: from the process-wide pinned cache (hipHostFree waits for
+// the whole device, so a save beside another index's build would stall on it)
 struct PinnedBuf {
     uint8_t* p = nullptr;
-    ~PinnedBuf() {
-        if (p) (void)hipHostFree(p);
-    }
+    size_t cap = 0;
+    ~PinnedBuf() { pinned_put(p, cap, false); }
 };
 
 constexpr size_t kIoChunk = (size_t)16 << 20;
@@ -3218,7 +3219,7 @@ int vsg_index_save(const vsg_index_t* h, const char* path) {
     // header placeholder, rewritten with the payload hash at the end
     if (std::fwrite(&fh, sizeof(fh), 1, fc.f) != 1) return fail(VSG_EINVAL, "write failed (header)");
     PinnedBuf buf;
-    HIP_TRY(hipHostMalloc((void**)&buf.p, kIoChunk, hipHostMallocDefault));
+    HIP_TRY(pinned_get(&buf.p, &buf.cap, kIoChunk, false));
     Fnv hash;
     hipStream_t st = h->stream;
     const std::vector<uint32_t> ring(h->free_ring.begin(), h->free_ring.end());
@@ -3302,7 +3303,7 @@ int vsg_index_load(const char* path, int device, vsg_index_t** out) {
     std::vector<uint32_t> upper_h(fh.upper_rows * fh.M);  // host copy for upper_levels_ok
     std::vector<uint32_t> ring(fh.version >= 2 ? s - fh.live : 0);
     PinnedBuf buf;
-    HIP_TRY(hipHostMalloc((void**)&buf.p, kIoChunk, hipHostMallocDefault));
+    HIP_TRY(pinned_get(&buf.p, &buf.cap, kIoChunk, false));
     Fnv hash;
     hipStream_t st = h->stream;
     const std::vector<Section> secs = sections(h, s, fh.upper_rows, ring.size(), fh.version);
@@ -3371,15 +3372,19 @@ int vsg_datagen_device(int kind, size_t n, size_t dim, uint64_t seed, uint64_t m
     if (kind < 0 || kind > 3 || dim == 0) return fail(VSG_EINVAL, "bad datagen arguments");
     hipStream_t s = (hipStream_t)stream;
     float *w = nullptr, *c = nullptr;
-    if (kind == 0 || kind == 3) {  // latent model scratch (small; freed after the stream drains)
-        HIP_TRY(hipMalloc((void**)&w, 64 * dim * 4));
-        HIP_TRY(hipMalloc((void**)&c, 1024 * 64 * 4));
+    if (kind == 0 || kind == 3) {  // latent model scratch (small; from the pool, freed in stream order)
+        hipError_t ea = dev_alloc(&w, 64 * dim, s);
+        if (ea == hipSuccess) ea = dev_alloc(&c, 1024 * 64, s);
+        if (ea != hipSuccess) {
+            dev_free(w, s);
+            return fail(VSG_ENOMEM, "datagen scratch");
+        }
     }
     const hipError_t e = launch_datagen(kind, n, dim, seed, model_seed, start_row, out, w, c, s);
     if (w) {
-        (void)hipStreamSynchronize(s);
-        (void)hipFree(w);
-        (void)hipFree(c);
+        dev_free(w, s);
+        dev_free(c, s);
+        (void)hipStreamSynchronize(s);  // the caller's stream only, as before
     }
     if (e != hipSuccess) return fail(VSG_EDEVICE, std::string("datagen: ") + hipGetErrorString(e));
     return VSG_OK;
